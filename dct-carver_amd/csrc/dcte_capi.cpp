@@ -1,0 +1,371 @@
+// dcte_capi.cpp -- C ABI of libdctenergy_hip.so (declared in include/dctenergy.h).
+//
+// Context = a set of devices; per device: lazily created stream, staging
+// buffers for the host entry point, and per-stream refinement scratch
+// (counter + list) so calls on different streams never share it.
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <map>
+#include <new>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/dctenergy.h"
+#include "dcte_kernels.h"
+#include "dcte_luma.h"
+
+namespace {
+
+constexpr double kDefaultTieTau = 4e-6;
+
+struct FixScratch {
+    unsigned* d_count = nullptr;   // pixels flagged for refinement
+    unsigned* d_list = nullptr;
+    size_t cap = 0;
+};
+
+struct Device {
+    int id = -1;
+    hipStream_t stream = nullptr;  // used by the host entry point
+    uint8_t* d_in = nullptr;
+    size_t in_cap = 0;
+    float* d_out = nullptr;
+    size_t out_cap = 0;
+    std::map<hipStream_t, FixScratch> fix;
+};
+
+}  // namespace
+
+struct ProfEvent {
+    int dev;
+    hipEvent_t a, b;
+};
+
+struct dcte_ctx {
+    std::vector<Device> devs;
+    double tie_tau = kDefaultTieTau;
+    bool profile = false;
+    std::vector<ProfEvent> prof;
+    long long last_refined = 0;
+    std::string last_error;
+};
+
+namespace {
+
+int hip_fail(dcte_ctx* ctx, hipError_t e, const char* where)
+{
+    ctx->last_error = std::string(where) + ": " + hipGetErrorString(e);
+    return e == hipErrorOutOfMemory ? DCTE_ENOMEM : DCTE_EHIP;
+}
+
+#define DCTE_HIP(ctx, expr)                                              \
+    do {                                                                 \
+        hipError_t e_ = (expr);                                          \
+        if (e_ != hipSuccess) return hip_fail((ctx), e_, #expr);         \
+    } while (0)
+
+bool valid_n(int n) { return n == 2 || n == 4 || n == 8 || n == 16; }
+
+// rows the clamp can touch for output rows [y0, y1)
+void needed_rows(int n, int h, int y0, int y1, int& lo, int& hi)
+{
+    int r = n / 2;
+    lo = y0 - (r - 1) < 0 ? 0 : y0 - (r - 1);
+    hi = y1 - 1 + r > h - 1 ? h - 1 : y1 - 1 + r;
+}
+
+int ensure_fix(dcte_ctx* ctx, Device& d, hipStream_t s, size_t npix, FixScratch** out)
+{
+    FixScratch& f = d.fix[s];
+    if (!f.d_count) {
+        DCTE_HIP(ctx, hipMalloc(&f.d_count, sizeof(unsigned)));
+        DCTE_HIP(ctx, hipMemset(f.d_count, 0, sizeof(unsigned)));
+    }
+    if (f.cap < npix) {
+        if (f.d_list) DCTE_HIP(ctx, hipFree(f.d_list));
+        f.d_list = nullptr;
+        f.cap = 0;
+        DCTE_HIP(ctx, hipMalloc(&f.d_list, npix * sizeof(unsigned)));
+        f.cap = npix;
+    }
+    *out = &f;
+    return DCTE_OK;
+}
+
+// the reference's makect (src/fft2d/fftsg.c:724-740) for nc = n, with libm,
+// exactly as the reference evaluates it; used by the fp64 refinement
+void small_twiddles(int n, double ct[4])
+{
+    ct[0] = ct[1] = ct[2] = ct[3] = 0.0;
+    if (n != 2 && n != 4) return;
+    int nch = n >> 1;
+    double delta = atan(1.0) / nch;
+    ct[0] = cos(delta * nch);
+    ct[nch] = 0.5 * ct[0];
+    for (int j = 1; j < nch; j++) {
+        ct[j] = 0.5 * cos(delta * j);
+        ct[n - j] = 0.5 * sin(delta * j);
+    }
+}
+
+int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, int w, int h,
+               int bpp, int in_row0, int in_rows, int y0, int y1, int n, float edges,
+               float textures, float* d_out, long long out_stride, hipStream_t s)
+{
+    if (!valid_n(n) || (bpp != 1 && bpp != 3) || w <= 0 || h <= 0) return DCTE_EINVAL;
+    if (y0 < 0 || y1 > h || y0 > y1 || !d_px || !d_out || out_stride < w) return DCTE_EINVAL;
+    if (rowstride < (long long)w * bpp) return DCTE_EINVAL;
+    if (y1 == y0) return DCTE_OK;
+    int lo, hi;
+    needed_rows(n, h, y0, y1, lo, hi);
+    if (lo < in_row0 || hi >= in_row0 + in_rows) return DCTE_EINVAL;
+    // one buffer resource addresses the readable rows: < 4 GiB
+    long long span = (long long)(in_rows - 1) * rowstride + (long long)w * bpp + 3;
+    if (span >= (1LL << 32)) return DCTE_ERANGE;
+    size_t npix = (size_t)(y1 - y0) * (size_t)w;
+    if (npix >= (1ULL << 32)) return DCTE_ERANGE;
+
+    DCTE_HIP(ctx, hipSetDevice(d.id));
+    FixScratch* f = nullptr;
+    int rc = ensure_fix(ctx, d, s, npix, &f);
+    if (rc) return rc;
+
+    const double scale = dcte::kLumaScale * (n >= 8 ? (double)n : 1.0);
+    dcte::MapParams p{};
+    p.px = static_cast<const uint8_t*>(d_px);
+    p.rowstride = rowstride;
+    p.w = w;
+    p.h = h;
+    p.in_row0 = in_row0;
+    p.in_rows = in_rows;
+    p.y0 = y0;
+    p.y1 = y1;
+    p.tile_h = dcte::map_default_tile_h(n);
+    p.out = d_out;
+    p.out_stride = out_stride;
+    p.we = (float)((double)edges / scale);
+    p.wt = (float)((double)textures / scale);
+    p.tie_tau = (float)ctx->tie_tau;
+    p.edges = edges;
+    p.textures = textures;
+    p.fix_count = f->d_count;
+    p.fix_list = f->d_list;
+    p.fix_cap = (unsigned)f->cap;
+
+    dcte::FixParams q{};
+    q.px = p.px;
+    q.rowstride = rowstride;
+    q.w = w;
+    q.h = h;
+    q.in_row0 = in_row0;
+    q.bpp = bpp;
+    q.n = n;
+    q.y0 = y0;
+    q.out = d_out;
+    q.out_stride = out_stride;
+    q.edges = edges;
+    q.textures = textures;
+    small_twiddles(n, q.ct);
+    q.fix_count = f->d_count;
+    q.fix_list = f->d_list;
+    q.fix_cap = (unsigned)f->cap;
+
+    DCTE_HIP(ctx, hipMemsetAsync(f->d_count, 0, sizeof(unsigned), s));
+    if (ctx->profile) {
+        ProfEvent ev{d.id, nullptr, nullptr};
+        DCTE_HIP(ctx, hipEventCreate(&ev.a));
+        DCTE_HIP(ctx, hipEventCreate(&ev.b));
+        DCTE_HIP(ctx, hipEventRecord(ev.a, s));
+        DCTE_HIP(ctx, dcte::launch_map(n, bpp, p, s));
+        DCTE_HIP(ctx, hipEventRecord(ev.b, s));
+        ctx->prof.push_back(ev);
+    } else {
+        DCTE_HIP(ctx, dcte::launch_map(n, bpp, p, s));
+    }
+    if ((p.we != p.wt && ctx->tie_tau > 0) || ctx->tie_tau >= 1.0)
+        DCTE_HIP(ctx, dcte::launch_fix(q, s));
+    return DCTE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dcte_abi_version(void) { return DCTE_ABI_VERSION; }
+
+int dcte_device_count(void)
+{
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) return 0;
+    return c;
+}
+
+int dcte_create(dcte_ctx** out, int ngpus, unsigned flags)
+{
+    (void)flags;
+    if (!out || ngpus < 0) return DCTE_EINVAL;
+    *out = nullptr;
+    int count = dcte_device_count();
+    if (count <= 0) return DCTE_ENODEV;
+    if (ngpus == 0 || ngpus > count) ngpus = count;
+    dcte_ctx* ctx = new (std::nothrow) dcte_ctx;
+    if (!ctx) return DCTE_ENOMEM;
+    ctx->devs.resize(ngpus);
+    for (int i = 0; i < ngpus; i++) ctx->devs[i].id = i;
+    const char* tau = getenv("DCTE_TIE_TAU");
+    if (tau && *tau) ctx->tie_tau = atof(tau);
+    *out = ctx;
+    return DCTE_OK;
+}
+
+void dcte_destroy(dcte_ctx* ctx)
+{
+    if (!ctx) return;
+    for (Device& d : ctx->devs) {
+        if (d.id < 0) continue;
+        if (hipSetDevice(d.id) != hipSuccess) continue;
+        if (d.stream) (void)hipStreamSynchronize(d.stream);
+        for (auto& kv : d.fix) {
+            (void)hipStreamSynchronize(kv.first);
+            if (kv.second.d_count) (void)hipFree(kv.second.d_count);
+            if (kv.second.d_list) (void)hipFree(kv.second.d_list);
+        }
+        if (d.d_in) (void)hipFree(d.d_in);
+        if (d.d_out) (void)hipFree(d.d_out);
+        if (d.stream) (void)hipStreamDestroy(d.stream);
+    }
+    delete ctx;
+}
+
+int dcte_ctx_devices(const dcte_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }
+
+int dcte_set_option(dcte_ctx* ctx, int option, double value)
+{
+    if (!ctx) return DCTE_EINVAL;
+    switch (option) {
+    case DCTE_OPT_TIE_TAU:
+        if (!(value >= 0)) return DCTE_EINVAL;
+        ctx->tie_tau = value;
+        return DCTE_OK;
+    case DCTE_OPT_PROFILE:
+        ctx->profile = value != 0;
+        return DCTE_OK;
+    default: return DCTE_EINVAL;
+    }
+}
+
+int dcte_energy_map_device(dcte_ctx* ctx, int device, const void* d_px, long long rowstride,
+                           int w, int h, int bpp, int in_row0, int in_rows, int y0, int y1,
+                           int n, float edges, float textures, float* d_out,
+                           long long out_stride, void* stream)
+{
+    if (!ctx || device < 0 || device >= (int)ctx->devs.size()) return DCTE_EINVAL;
+    return run_device(ctx, ctx->devs[device], d_px, rowstride, w, h, bpp, in_row0, in_rows, y0,
+                      y1, n, edges, textures, d_out, out_stride, (hipStream_t)stream);
+}
+
+int dcte_energy_map(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride,
+                    int n, float edges, float textures, int semantics, int transposed, float* out)
+{
+    if (!ctx || !px || !out) return DCTE_EINVAL;
+    if (!valid_n(n) || (bpp != 1 && bpp != 3) || w <= 0 || h <= 0) return DCTE_EINVAL;
+    if (rowstride < (size_t)w * bpp) return DCTE_EINVAL;
+    if (semantics != DCTE_LQR) return semantics == DCTE_PREVIEW ? DCTE_ENOTSUP : DCTE_EINVAL;
+    if (transposed) return DCTE_ENOTSUP;
+    const int G = (int)ctx->devs.size() < h ? (int)ctx->devs.size() : h;
+    const size_t pitch = (size_t)w * bpp;
+    ctx->last_refined = 0;
+    // bands: device k computes rows [k*h/G, (k+1)*h/G) from its band + halo
+    for (int k = 0; k < G; k++) {
+        Device& d = ctx->devs[k];
+        int y0 = (int)((long long)h * k / G), y1 = (int)((long long)h * (k + 1) / G);
+        int lo, hi;
+        needed_rows(n, h, y0, y1, lo, hi);
+        size_t in_bytes = pitch * (size_t)(hi - lo + 1);
+        size_t out_bytes = sizeof(float) * (size_t)w * (size_t)(y1 - y0);
+        DCTE_HIP(ctx, hipSetDevice(d.id));
+        if (!d.stream) DCTE_HIP(ctx, hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+        if (d.in_cap < in_bytes) {
+            if (d.d_in) DCTE_HIP(ctx, hipFree(d.d_in));
+            d.d_in = nullptr;
+            d.in_cap = 0;
+            DCTE_HIP(ctx, hipMalloc(&d.d_in, in_bytes));
+            d.in_cap = in_bytes;
+        }
+        if (d.out_cap < out_bytes) {
+            if (d.d_out) DCTE_HIP(ctx, hipFree(d.d_out));
+            d.d_out = nullptr;
+            d.out_cap = 0;
+            DCTE_HIP(ctx, hipMalloc(&d.d_out, out_bytes));
+            d.out_cap = out_bytes;
+        }
+        DCTE_HIP(ctx, hipMemcpy2DAsync(d.d_in, pitch, px + (size_t)lo * rowstride, rowstride,
+                                       pitch, hi - lo + 1, hipMemcpyHostToDevice, d.stream));
+        int rc = run_device(ctx, d, d.d_in, (long long)pitch, w, h, bpp, lo, hi - lo + 1, y0, y1,
+                            n, edges, textures, d.d_out, w, d.stream);
+        if (rc) return rc;
+        DCTE_HIP(ctx, hipMemcpyAsync(out + (size_t)y0 * w, d.d_out, out_bytes,
+                                     hipMemcpyDeviceToHost, d.stream));
+    }
+    for (int k = 0; k < G; k++) {
+        Device& d = ctx->devs[k];
+        DCTE_HIP(ctx, hipSetDevice(d.id));
+        DCTE_HIP(ctx, hipStreamSynchronize(d.stream));
+        auto it = d.fix.find(d.stream);
+        if (it != d.fix.end()) {
+            unsigned cnt = 0;
+            DCTE_HIP(ctx, hipMemcpy(&cnt, it->second.d_count, sizeof(unsigned), hipMemcpyDeviceToHost));
+            ctx->last_refined += cnt;
+        }
+    }
+    return DCTE_OK;
+}
+
+int dcte_profile_read(dcte_ctx* ctx, long long* launches, double* kernel_ms)
+{
+    if (!ctx || !launches || !kernel_ms) return DCTE_EINVAL;
+    double total = 0.0;
+    int rc = DCTE_OK;
+    for (ProfEvent& ev : ctx->prof) {
+        if (rc == DCTE_OK) {
+            float ms = 0.0f;
+            hipError_t e = hipSetDevice(ev.dev);
+            if (e == hipSuccess) e = hipEventSynchronize(ev.b);
+            if (e == hipSuccess) e = hipEventElapsedTime(&ms, ev.a, ev.b);
+            if (e != hipSuccess) rc = hip_fail(ctx, e, "dcte_profile_read");
+            total += ms;
+        }
+        (void)hipEventDestroy(ev.a);
+        (void)hipEventDestroy(ev.b);
+    }
+    *launches = (long long)ctx->prof.size();
+    *kernel_ms = total;
+    ctx->prof.clear();
+    return rc;
+}
+
+long long dcte_last_refined(const dcte_ctx* ctx) { return ctx ? ctx->last_refined : 0; }
+
+const char* dcte_strerror(int code)
+{
+    switch (code) {
+    case DCTE_OK: return "success";
+    case DCTE_EINVAL: return "invalid argument";
+    case DCTE_ENODEV: return "no HIP device";
+    case DCTE_ENOMEM: return "out of memory";
+    case DCTE_EHIP: return "HIP runtime error";
+    case DCTE_ERANGE: return "frame too large for one launch";
+    case DCTE_ENOTSUP: return "not supported by this build";
+    default: return "unknown error";
+    }
+}
+
+const char* dcte_last_error(const dcte_ctx* ctx) { return ctx ? ctx->last_error.c_str() : ""; }
+
+}  // extern "C"

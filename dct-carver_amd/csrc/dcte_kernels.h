@@ -1,0 +1,54 @@
+// dcte_kernels.h -- launch-side view of the energy-map kernels (no HIP types
+// leak into the public C ABI; this header is internal to libdctenergy_hip).
+#pragma once
+
+#include <stdint.h>
+
+#include <hip/hip_runtime.h>
+
+namespace dcte {
+
+// One launch computes output rows [y0, y1) of a w x h image.  The input
+// pointer addresses global row `in_row0`; rows [in_row0, in_row0 + in_rows)
+// are readable.  Every row the window clamp can touch for [y0, y1)
+// (clamp(y0 - N/2 + 1) .. clamp(y1 - 1 + N/2)) must be readable: a row band
+// plus its halo, or the whole frame.
+struct MapParams {
+    const uint8_t* px;
+    long long rowstride;     // bytes
+    int w, h;                // global image size
+    int in_row0, in_rows;    // readable input rows (global)
+    int y0, y1;              // output rows (global)
+    int tile_h;              // output rows per workgroup
+    float* out;              // row y at out + (y - y0) * out_stride
+    long long out_stride;    // floats
+    float we, wt;            // edges / textures weights, pre-scaled to luma units
+    float tie_tau;           // relative edge/texture margin sent to refinement
+    float edges, textures;   // raw weights (refinement path)
+    unsigned* fix_count;     // refinement list (pixel = (y - y0) * w + x)
+    unsigned* fix_list;
+    unsigned fix_cap;
+};
+
+struct FixParams {
+    const uint8_t* px;
+    long long rowstride;
+    int w, h, in_row0, bpp, n, y0;
+    float* out;
+    long long out_stride;
+    float edges, textures;
+    double ct[4];            // makect twiddles (N = 2, 4)
+    unsigned* fix_count;     // pixels flagged by the map kernel
+    unsigned* fix_list;
+    unsigned fix_cap;
+};
+
+// host-side launchers (dcte_kernels.hip)
+hipError_t launch_map(int n, int bpp, const MapParams& p, hipStream_t s);
+hipError_t launch_fix(const FixParams& p, hipStream_t s);
+
+// geometry the launcher uses (exported for tests / bench)
+int map_tile_w(int n);
+int map_default_tile_h(int n);
+
+}  // namespace dcte

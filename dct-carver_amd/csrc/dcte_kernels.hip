@@ -1,0 +1,247 @@
+// dcte_kernels.hip -- gfx950 kernels for the dct-carver energy map.
+//
+// What is computed (reference: src/render.c:134-157 + src/dct.c:93-126):
+// for every pixel (x, y) the N x N luma window with offsets -(N/2-1)..N/2 in
+// both axes (replicate-clamped at the image border), its 2-D DCT-II, and
+//     E = m_e > m_t ? m_e * edges : m_t * textures
+// with m_e = max(|C01|, |C10|) and m_t = max over the other non-DC
+// coefficients -- the reference's last-maximum scan reduced to a comparison
+// (SURVEY.md §0.5).
+//
+// How (VALU-bound design, no MFMA -- see DESIGN.md §3):
+//  * A workgroup owns a strip of TW output columns x tile_h output rows and
+//    walks DOWN it.  Each input row is DCT-transformed along x exactly once
+//    (row pass) and kept in a register ring of the last N row transforms;
+//    every output pixel then only needs the N column transforms over the
+//    ring (N + 1 one-dimensional transforms per pixel instead of 2N).
+//  * Pixels arrive as raw bytes: one 32-bit buffer load per lane per row
+//    (bounds-checked buffer resource, no over-read), prefetched one group of
+//    G rows ahead in registers, staged through LDS, converted to the exact
+//    integer luma domain (dcte_luma.h), staged again, and read back as the
+//    N-wide row windows.  Two barriers per group of G rows.
+//  * N = 16 splits the 16 horizontal frequencies of a column over two lanes
+//    (even / odd k1) to keep the ring at 8 x 16 registers per lane.
+//  * Pixels whose edge/texture decision falls inside the fp32 error band are
+//    appended to a list and recomputed by dcte_fix in fp64, in the
+//    reference's operation order.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <utility>
+
+#include "dcte_kernels.h"
+#include "dcte_luma.h"
+#include "dcte_math.h"
+#include "dcte_passes.h"
+#include "dcte_ref64.h"
+
+namespace dcte {
+
+constexpr int kThreads = 256;
+constexpr unsigned kBufFlags = 0x00020000u;  // gfx9 raw buffer dword3
+
+template <int N>
+struct Geo {
+    static constexpr int S = Lanes<N>::S;                // lanes per output column
+    static constexpr int CH = Lanes<N>::CH;              // k1 channels per lane
+    static constexpr int TW = kThreads / S;              // output columns per WG
+    static constexpr int HL = N / 2 - 1;                 // halo left / top
+    static constexpr int HR = N / 2;                     // halo right / bottom
+    static constexpr int LW = TW + N - 1;                // luma columns per row
+    static constexpr int LWP = LW + 1;
+    static constexpr int G = (N < 8) ? 8 : N;            // rows per group (multiple of N)
+    template <int BPP>
+    static constexpr int ndw() { return (LW * BPP + 3) / 4 + 1; }  // dwords per raw row
+};
+
+template <int... Is, class F>
+__device__ __forceinline__ void static_for_impl(std::integer_sequence<int, Is...>, F&& f)
+{
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int Count, class F>
+__device__ __forceinline__ void static_for(F&& f)
+{
+    static_for_impl(std::make_integer_sequence<int, Count>{}, f);
+}
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// ------------------------------------------------------------------ main kernel
+template <int N, int BPP>
+__global__ __launch_bounds__(kThreads) void dcte_map(const MapParams p)
+{
+    using Gm = Geo<N>;
+    constexpr int S = Gm::S, CH = Gm::CH, TW = Gm::TW, HL = Gm::HL;
+    constexpr int LW = Gm::LW, LWP = Gm::LWP, G = Gm::G;
+    constexpr int NDW = Gm::template ndw<BPP>();
+    static_assert(NDW <= kThreads, "one raw dword per lane per row");
+
+    __shared__ uint32_t raw[G][NDW];
+    __shared__ float lum[G][LWP];
+
+    const int tx = threadIdx.x;
+    const int lane_p = (S == 2) ? (tx & 1) : 0;
+    const int c = (S == 2) ? (tx >> 1) : tx;         // output column within the strip
+    const int x0 = blockIdx.x * TW;
+    const int x = x0 + c;
+    const int ys = p.y0 + blockIdx.y * p.tile_h;
+    const int ye = min(ys + p.tile_h, p.y1);
+    const int n_in = (ye - ys) + N - 1;
+    const int ngroups = (n_in + G - 1) / G;
+    const int w = p.w, h = p.h;
+
+    // raw byte span of one input row: columns [xs, xs + span) of the strip
+    const int xs = max(0, x0 - HL);
+    // buffer resource over the readable rows (aligned base; OOB loads read 0)
+    const uintptr_t pbase = reinterpret_cast<uintptr_t>(p.px);
+    const uint32_t base_off = (uint32_t)(pbase & 3u);
+    const unsigned nrec = base_off + (unsigned)((long long)(p.in_rows - 1) * p.rowstride) +
+                          (unsigned)(w * BPP);
+    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(pbase - base_off), (short)0, (int)nrec, (int)kBufFlags);
+
+    auto row_start = [&](int i) -> uint32_t {       // byte offset of (xs, row i)
+        int t = clampi(ys - HL + i, 0, h - 1);
+        return base_off + (uint32_t)((long long)(t - p.in_row0) * p.rowstride) +
+               (uint32_t)(xs * BPP);
+    };
+
+    uint32_t pref[G];
+    auto issue = [&](int g) {
+#pragma unroll
+        for (int u = 0; u < G; u++) {
+            int i = g * G + u;
+            uint32_t a = row_start(i < n_in ? i : n_in - 1) & ~3u;
+            pref[u] = (tx < NDW) ? __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * tx), 0, 0) : 0u;
+        }
+    };
+
+    float ring[N][CH];
+    float we = p.we, wt = p.wt;
+
+    issue(0);
+    for (int g = 0; g < ngroups; g++) {
+        // stage raw bytes of group g, then prefetch group g + 1
+        if (tx < NDW) {
+#pragma unroll
+            for (int u = 0; u < G; u++) raw[u][tx] = pref[u];
+        }
+        if (g + 1 < ngroups) issue(g + 1);
+        __syncthreads();
+        // bytes -> exact integer luma (biased), one column per lane (+ halo)
+        for (int cc = tx; cc < LW; cc += kThreads) {
+            int xc = clampi(x0 - HL + cc, 0, w - 1);
+#pragma unroll
+            for (int u = 0; u < G; u++) {
+                uint32_t rs = row_start(g * G + u);
+                uint32_t off = (rs & 3u) + (uint32_t)((xc - xs) * BPP);
+                const uint8_t* rb = reinterpret_cast<const uint8_t*>(&raw[u][0]);
+                int L;
+                if constexpr (BPP == 1) {
+                    L = kLumaGrey * (int)rb[off];
+                } else {
+                    L = kLumaR * (int)rb[off] + kLumaG * (int)rb[off + 1] + kLumaB * (int)rb[off + 2];
+                }
+                lum[u][cc] = (float)(L - kLumaBias);
+            }
+        }
+        __syncthreads();
+        // row pass + column pass for the G rows of this group
+        static_for<G>([&](auto U) {
+            constexpr int u = decltype(U)::value;
+            const int i = g * G + u;
+            if (i < n_in) {
+                row_pass<N>(&lum[u][0], c, lane_p, ring[u % N]);
+                if (i >= N - 1) {
+                    float mt, me;
+                    Cols<N>::template run<(u + 1) % N>(ring, lane_p, mt, me);
+                    if constexpr (S == 2) {
+                        mt = fmaxf(mt, __shfl_xor(mt, 1));
+                        me = fmaxf(me, __shfl_xor(me, 1));
+                    }
+                    const int y = ys + i - (N - 1);
+                    if (x < w && lane_p == 0) {
+                        const bool edge = me > mt;
+                        p.out[(long long)(y - p.y0) * p.out_stride + x] = edge ? me * we : mt * wt;
+                        // refine in fp64 when the class is uncertain (or, for
+                        // testing, tie_tau >= 1: every pixel)
+                        const float hi = fmaxf(me, mt);
+                        if ((we != wt && hi > 0.0f && fabsf(me - mt) <= p.tie_tau * hi) ||
+                            p.tie_tau >= 1.0f) {
+                            unsigned k = atomicAdd(p.fix_count, 1u);
+                            if (k < p.fix_cap) p.fix_list[k] = (unsigned)((y - p.y0) * w + x);
+                        }
+                    }
+                }
+            }
+        });
+    }
+}
+
+// ------------------------------------------------------------------ refinement
+template <int N>
+__global__ __launch_bounds__(64) void dcte_fix(const FixParams p)
+{
+    const unsigned cnt = min(*p.fix_count, p.fix_cap);
+    constexpr int r = N / 2;
+    for (unsigned k = blockIdx.x * blockDim.x + threadIdx.x; k < cnt; k += gridDim.x * blockDim.x) {
+        const unsigned idx = p.fix_list[k];
+        const int y = p.y0 + (int)(idx / (unsigned)p.w);
+        const int x = (int)(idx % (unsigned)p.w);
+        double d[N * N];
+        for (int i = -r + 1; i <= r; i++) {
+            const int xx = clampi(x + i, 0, p.w - 1);
+            for (int j = -r + 1; j <= r; j++) {
+                const int yy = clampi(y + j, 0, p.h - 1);
+                const uint8_t* px = p.px + (long long)(yy - p.in_row0) * p.rowstride + (long long)xx * p.bpp;
+                d[(i + r - 1) * N + (j + r - 1)] = r64::luma(px, p.bpp);
+            }
+        }
+        r64::transform(N, d, p.ct);
+        p.out[(long long)(y - p.y0) * p.out_stride + x] = r64::weighted_max(N, d, p.edges, p.textures);
+    }
+}
+
+// ------------------------------------------------------------------ launchers
+int map_tile_w(int n) { return n == 16 ? Geo<16>::TW : kThreads; }
+int map_default_tile_h(int n) { return n == 16 ? 128 : 128; }
+
+template <int N, int BPP>
+static hipError_t launch_map_t(const MapParams& p, hipStream_t s)
+{
+    dim3 grid((p.w + Geo<N>::TW - 1) / Geo<N>::TW, (p.y1 - p.y0 + p.tile_h - 1) / p.tile_h);
+    hipLaunchKernelGGL((dcte_map<N, BPP>), grid, dim3(kThreads), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_map(int n, int bpp, const MapParams& p, hipStream_t s)
+{
+    if (p.y1 <= p.y0) return hipSuccess;
+#define DCTE_CASE(NN)                                                          \
+    case NN:                                                                   \
+        return bpp == 1 ? launch_map_t<NN, 1>(p, s) : launch_map_t<NN, 3>(p, s);
+    switch (n) {
+        DCTE_CASE(2)
+        DCTE_CASE(4)
+        DCTE_CASE(8)
+        DCTE_CASE(16)
+    default: return hipErrorInvalidValue;
+    }
+#undef DCTE_CASE
+}
+
+hipError_t launch_fix(const FixParams& p, hipStream_t s)
+{
+    dim3 grid(256), block(64);
+    switch (p.n) {
+    case 2: hipLaunchKernelGGL(dcte_fix<2>, grid, block, 0, s, p); break;
+    case 4: hipLaunchKernelGGL(dcte_fix<4>, grid, block, 0, s, p); break;
+    case 8: hipLaunchKernelGGL(dcte_fix<8>, grid, block, 0, s, p); break;
+    case 16: hipLaunchKernelGGL(dcte_fix<16>, grid, block, 0, s, p); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace dcte

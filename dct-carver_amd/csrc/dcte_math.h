@@ -1,0 +1,202 @@
+// dcte_math.h -- fp32 transform arithmetic of the energy-map kernels.
+//
+// Shared, unchanged, by the gfx950 kernels (dcte_kernels.hip) and by the
+// host-side emulation used in tests (tests/emu/), so that CPU tests can check
+// the exact fp32 operation sequence the GPU runs.  Both sides compile with
+// -ffp-contract=off and every fused multiply-add is an explicit fmaf(), so
+// host and device results are bit-identical.
+//
+// Units ("hat" scaling).  A 1-D transform of length N returns
+//     X[0] = sum_j x_j                         (unscaled DC)
+//     X[k] = g * sum_j x_j cos(pi (2j+1) k / 2N),   k >= 1
+// with g = sqrt(2) for the orthonormal family (N = 8, 16: ddct8x8s /
+// ddct16x16s, src/fft2d/shrtdct.c:18-28,189-193) and g = 1 for the
+// unnormalised family (N = 2, 4: ddct2d, src/fft2d/fftsg2d.c:204-209).
+// Then every 2-D coefficient is C[k1][k2] * S with one global S (N for the
+// orthonormal family, 1 for the unnormalised one), so comparisons between
+// coefficients -- all that the weighted max needs (src/dct.c:112-126) -- are
+// unaffected, and the kernel folds 1/S and the luma scale into the weights.
+//
+// Exactness.  Inputs are integer-valued luma samples biased into
+// [-637500, 637500] (dcte_luma.h), so every sum/difference of the first
+// butterfly stages is an exact fp32 integer (< 2^24).  Rounding therefore only
+// enters through the rotations, whose operands scale with the window's local
+// contrast, never with its mean brightness.  The DC column (k1 = 0) of the
+// second pass is kept free of large partial sums (see col_dc_*).
+#pragma once
+
+#include <math.h>
+
+#if defined(__HIPCC__)
+#define DCTE_HD __host__ __device__ __forceinline__
+#else
+#define DCTE_HD static inline
+#endif
+
+namespace dcte {
+
+// ---------------------------------------------------------------- N = 8
+// g * cos(pi (2j+1) k / 16) magnitudes (g = sqrt 2)
+constexpr float k8A = 1.3870398453221475f;   // cos(1 pi/16)
+constexpr float k8B = 1.1758756024193588f;   // cos(3 pi/16)
+constexpr float k8C = 0.7856949583871023f;   // cos(5 pi/16)
+constexpr float k8D = 0.2758993792829431f;   // cos(7 pi/16)
+constexpr float k8E = 1.3065629648763766f;   // cos(2 pi/16)
+constexpr float k8F = 0.5411961001461971f;   // cos(6 pi/16)
+
+// odd outputs X1, X3, X5, X7 from d_j = x_j - x_{7-j}
+DCTE_HD void dct8_odd(float d0, float d1, float d2, float d3,
+                      float& X1, float& X3, float& X5, float& X7)
+{
+    X1 = fmaf(d3, k8D, fmaf(d2, k8C, fmaf(d1, k8B, d0 * k8A)));
+    X3 = fmaf(d3, -k8C, fmaf(d2, -k8A, fmaf(d1, -k8D, d0 * k8B)));
+    X5 = fmaf(d3, k8B, fmaf(d2, k8D, fmaf(d1, -k8A, d0 * k8C)));
+    X7 = fmaf(d3, -k8A, fmaf(d2, k8B, fmaf(d1, -k8C, d0 * k8D)));
+}
+
+// full 8-point transform (first pass, and k1 >= 1 columns of the second)
+DCTE_HD void dct8(const float x[8], float X[8])
+{
+    float s0 = x[0] + x[7], d0 = x[0] - x[7];
+    float s1 = x[1] + x[6], d1 = x[1] - x[6];
+    float s2 = x[2] + x[5], d2 = x[2] - x[5];
+    float s3 = x[3] + x[4], d3 = x[3] - x[4];
+    float a = s0 + s3, b = s1 + s2, c = s0 - s3, e = s1 - s2;
+    X[0] = a + b;
+    X[4] = a - b;
+    X[2] = fmaf(c, k8E, e * k8F);
+    X[6] = fmaf(c, k8F, -(e * k8E));
+    dct8_odd(d0, d1, d2, d3, X[1], X[3], X[5], X[7]);
+}
+
+// max over |X[0..7]| of a column whose 8 outputs are all texture atoms,
+// folded into m.  max(|a+b|, |a-b|) = |a| + |b| replaces X0 and X4.
+DCTE_HD float dct8_tex_max(const float x[8], float m)
+{
+    float s0 = x[0] + x[7], d0 = x[0] - x[7];
+    float s1 = x[1] + x[6], d1 = x[1] - x[6];
+    float s2 = x[2] + x[5], d2 = x[2] - x[5];
+    float s3 = x[3] + x[4], d3 = x[3] - x[4];
+    float a = s0 + s3, b = s1 + s2, c = s0 - s3, e = s1 - s2;
+    float X04 = fabsf(a) + fabsf(b);
+    float X2 = fmaf(c, k8E, e * k8F);
+    float X6 = fmaf(c, k8F, -(e * k8E));
+    float X1, X3, X5, X7;
+    dct8_odd(d0, d1, d2, d3, X1, X3, X5, X7);
+    m = fmaxf(fmaxf(m, X04), fabsf(X2));
+    m = fmaxf(fmaxf(m, fabsf(X6)), fabsf(X1));
+    m = fmaxf(fmaxf(m, fabsf(X3)), fabsf(X5));
+    return fmaxf(m, fabsf(X7));
+}
+
+// k1 = 1 column: X[0] is the edge atom (1,0); X[1..7] are textures.
+DCTE_HD float dct8_k1_max(const float x[8], float m, float& edge)
+{
+    float s0 = x[0] + x[7], d0 = x[0] - x[7];
+    float s1 = x[1] + x[6], d1 = x[1] - x[6];
+    float s2 = x[2] + x[5], d2 = x[2] - x[5];
+    float s3 = x[3] + x[4], d3 = x[3] - x[4];
+    float a = s0 + s3, b = s1 + s2, c = s0 - s3, e = s1 - s2;
+    edge = fabsf(a + b);
+    float X4 = a - b;
+    float X2 = fmaf(c, k8E, e * k8F);
+    float X6 = fmaf(c, k8F, -(e * k8E));
+    float X1, X3, X5, X7;
+    dct8_odd(d0, d1, d2, d3, X1, X3, X5, X7);
+    m = fmaxf(fmaxf(m, fabsf(X4)), fabsf(X2));
+    m = fmaxf(fmaxf(m, fabsf(X6)), fabsf(X1));
+    m = fmaxf(fmaxf(m, fabsf(X3)), fabsf(X5));
+    return fmaxf(m, fabsf(X7));
+}
+
+// k1 = 0 column (inputs: exact integer row sums, |x| <= 5.1e6).  X[0] (the
+// DC, unused) is never formed; X4 = (s0 - s1) + (s3 - s2) avoids the large
+// partial sums a = s0 + s3, b = s1 + s2.  X[1] is the edge atom (0,1).
+DCTE_HD float dct8_k0_max(const float x[8], float m, float& edge)
+{
+    float s0 = x[0] + x[7], d0 = x[0] - x[7];
+    float s1 = x[1] + x[6], d1 = x[1] - x[6];
+    float s2 = x[2] + x[5], d2 = x[2] - x[5];
+    float s3 = x[3] + x[4], d3 = x[3] - x[4];
+    float c = s0 - s3, e = s1 - s2;
+    float X4 = (s0 - s1) + (s3 - s2);
+    float X2 = fmaf(c, k8E, e * k8F);
+    float X6 = fmaf(c, k8F, -(e * k8E));
+    float X1, X3, X5, X7;
+    dct8_odd(d0, d1, d2, d3, X1, X3, X5, X7);
+    edge = fabsf(X1);
+    m = fmaxf(fmaxf(m, fabsf(X4)), fabsf(X2));
+    m = fmaxf(fmaxf(m, fabsf(X6)), fabsf(X3));
+    return fmaxf(fmaxf(m, fabsf(X5)), fabsf(X7));
+}
+
+// ---------------------------------------------------------------- N = 4, 2
+// unnormalised family (g = 1): cos(pi/4), cos(pi/8), cos(3 pi/8)
+constexpr float k4H = 0.7071067811865476f;
+constexpr float k4A = 0.9238795325112867f;
+constexpr float k4B = 0.38268343236508984f;
+
+DCTE_HD void dct4(const float x[4], float X[4])
+{
+    float s0 = x[0] + x[3], d0 = x[0] - x[3];
+    float s1 = x[1] + x[2], d1 = x[1] - x[2];
+    X[0] = s0 + s1;
+    X[2] = (s0 - s1) * k4H;
+    X[1] = fmaf(d1, k4B, d0 * k4A);
+    X[3] = fmaf(d1, -k4A, d0 * k4B);
+}
+
+DCTE_HD void dct2(const float x[2], float X[2])
+{
+    X[0] = x[0] + x[1];
+    X[1] = (x[0] - x[1]) * k4H;
+}
+
+// ---------------------------------------------------------------- N = 16
+// odd-part matrix g * cos(pi (2j+1) k / 32), k odd, j = 0..7 (g = sqrt 2)
+constexpr float k16a0 = 1.4074037375263826f;  // cos( 1 pi/32)
+constexpr float k16a1 = 1.3533180011743526f;  // cos( 3 pi/32)
+constexpr float k16a2 = 1.2472250129866713f;  // cos( 5 pi/32)
+constexpr float k16a3 = 1.0932018670017576f;  // cos( 7 pi/32)
+constexpr float k16a4 = 0.8971675863426364f;  // cos( 9 pi/32)
+constexpr float k16a5 = 0.6666556584777468f;  // cos(11 pi/32)
+constexpr float k16a6 = 0.41052452752235735f; // cos(13 pi/32)
+constexpr float k16a7 = 0.1386171691990917f;  // cos(15 pi/32)
+
+// X[2m+1] = sum_j d_j * sign * a_{|...|}; the 8 x 8 sign/index table of
+// cos(pi (2j+1)(2m+1)/32) folded onto the eight magnitudes above.
+DCTE_HD void dct16_odd(const float d[8], float X[16])
+{
+    const float A0 = k16a0, A1 = k16a1, A2 = k16a2, A3 = k16a3;
+    const float A4 = k16a4, A5 = k16a5, A6 = k16a6, A7 = k16a7;
+#define DCTE_ROW(o, c0, c1, c2, c3, c4, c5, c6, c7)                                   \
+    X[o] = fmaf(d[7], c7, fmaf(d[6], c6, fmaf(d[5], c5, fmaf(d[4], c4,                \
+           fmaf(d[3], c3, fmaf(d[2], c2, fmaf(d[1], c1, d[0] * c0)))))));
+    DCTE_ROW(1,  A0,  A1,  A2,  A3,  A4,  A5,  A6,  A7)
+    DCTE_ROW(3,  A1,  A4,  A7, -A5, -A2, -A0, -A3, -A6)
+    DCTE_ROW(5,  A2,  A7, -A3, -A1, -A6,  A4,  A0,  A5)
+    DCTE_ROW(7,  A3, -A5, -A1,  A7,  A0,  A6, -A2, -A4)
+    DCTE_ROW(9,  A4, -A2, -A6,  A0, -A7, -A1,  A5,  A3)
+    DCTE_ROW(11, A5, -A0,  A4,  A6, -A1,  A3,  A7, -A2)
+    DCTE_ROW(13, A6, -A3,  A0, -A2,  A5,  A7, -A4,  A1)
+    DCTE_ROW(15, A7, -A6,  A5, -A4,  A3, -A2,  A1, -A0)
+#undef DCTE_ROW
+}
+
+// full 16-point transform: even half = 8-point transform of s_j = x_j + x_{15-j}
+// (same g), odd half from d_j = x_j - x_{15-j}.
+DCTE_HD void dct16(const float x[16], float X[16])
+{
+    float s[8], d[8], E[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        s[j] = x[j] + x[15 - j];
+        d[j] = x[j] - x[15 - j];
+    }
+    dct8(s, E);
+#pragma unroll
+    for (int m = 0; m < 8; m++) X[2 * m] = E[m];
+    dct16_odd(d, X);
+}
+
+}  // namespace dcte

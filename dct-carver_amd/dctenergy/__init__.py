@@ -1,0 +1,219 @@
+"""dctenergy -- Python binding of libdctenergy_hip.so (the MI355X energy-map backend).
+
+The product is the C ABI in include/dctenergy.h; this module is a thin ctypes
+view of it for tests, the bench and Python callers.  There is no CPU fallback:
+if the HIP library is missing or no device is present, every entry point
+raises (the reference's CPU path lives only in oracle/, as the checker).
+
+Reference interface mirrored (avivrosenberg/dct-carver):
+  * Context.energy_map     <- W*H calls of dct_pixel_energy (src/render.c:134-157)
+  * carver.EnergyParameters / init_carver_from_vals / dct_pixel_energy
+                           <- src/render.h:9-18, src/render.c:286-325
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get(
+    "DCTE_LIB", os.path.join(os.path.dirname(_HERE), "build", "libdctenergy_hip.so"))
+
+DCTE_OK = 0
+DCTE_EINVAL = -1
+DCTE_ENODEV = -2
+DCTE_ENOMEM = -3
+DCTE_EHIP = -4
+DCTE_ERANGE = -5
+DCTE_ENOTSUP = -6
+
+DCTE_LQR = 0
+DCTE_PREVIEW = 1
+DCTE_OPT_TIE_TAU = 1
+DCTE_OPT_PROFILE = 2
+
+# every symbol include/dctenergy.h declares
+EXPORTS = ("dcte_abi_version", "dcte_device_count", "dcte_create", "dcte_destroy",
+           "dcte_ctx_devices", "dcte_set_option", "dcte_energy_map",
+           "dcte_energy_map_device", "dcte_last_refined", "dcte_profile_read", "dcte_strerror",
+           "dcte_last_error")
+
+_lib = None
+
+
+class DcteError(RuntimeError):
+    def __init__(self, code, detail=""):
+        self.code = code
+        msg = f"dctenergy error {code}: {_strerror(code)}"
+        if detail:
+            msg += f" ({detail})"
+        super().__init__(msg)
+
+
+def _strerror(code):
+    try:
+        return lib().dcte_strerror(code).decode()
+    except OSError:
+        return "library not loaded"
+
+
+def lib():
+    """Load libdctenergy_hip.so (raises OSError when it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OSError(f"libdctenergy_hip.so not found at {LIB_PATH}; run __graft_entry__.build()")
+    L = ctypes.CDLL(LIB_PATH)
+    vp = ctypes.c_void_p
+    L.dcte_abi_version.restype = ctypes.c_int
+    L.dcte_device_count.restype = ctypes.c_int
+    L.dcte_create.restype = ctypes.c_int
+    L.dcte_create.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_uint]
+    L.dcte_destroy.restype = None
+    L.dcte_destroy.argtypes = [vp]
+    L.dcte_ctx_devices.restype = ctypes.c_int
+    L.dcte_ctx_devices.argtypes = [vp]
+    L.dcte_set_option.restype = ctypes.c_int
+    L.dcte_set_option.argtypes = [vp, ctypes.c_int, ctypes.c_double]
+    L.dcte_energy_map.restype = ctypes.c_int
+    L.dcte_energy_map.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_size_t, ctypes.c_int, ctypes.c_float,
+                                  ctypes.c_float, ctypes.c_int, ctypes.c_int, vp]
+    L.dcte_energy_map_device.restype = ctypes.c_int
+    L.dcte_energy_map_device.argtypes = [vp, ctypes.c_int, vp, ctypes.c_longlong, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                         ctypes.c_float, vp, ctypes.c_longlong, vp]
+    L.dcte_last_refined.restype = ctypes.c_longlong
+    L.dcte_last_refined.argtypes = [vp]
+    L.dcte_profile_read.restype = ctypes.c_int
+    L.dcte_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_longlong),
+                                    ctypes.POINTER(ctypes.c_double)]
+    L.dcte_strerror.restype = ctypes.c_char_p
+    L.dcte_strerror.argtypes = [ctypes.c_int]
+    L.dcte_last_error.restype = ctypes.c_char_p
+    L.dcte_last_error.argtypes = [vp]
+    _lib = L
+    return L
+
+
+def device_count():
+    return lib().dcte_device_count()
+
+
+class Context:
+    """One dcte_ctx (a set of devices).  Not thread-safe, like the reference
+    callback (src/render.c:140 shares params->data)."""
+
+    def __init__(self, ngpus=0, tie_tau=None):
+        L = lib()
+        h = ctypes.c_void_p()
+        rc = L.dcte_create(ctypes.byref(h), ngpus, 0)
+        if rc != DCTE_OK:
+            raise DcteError(rc)
+        self._h = h
+        if tie_tau is not None:
+            self.set_option(DCTE_OPT_TIE_TAU, tie_tau)
+
+    # -- lifecycle
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().dcte_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc):
+        if rc != DCTE_OK:
+            raise DcteError(rc, lib().dcte_last_error(self._h).decode())
+
+    @property
+    def ndevices(self):
+        return lib().dcte_ctx_devices(self._h)
+
+    @property
+    def last_refined(self):
+        return lib().dcte_last_refined(self._h)
+
+    def set_option(self, opt, value):
+        self._check(lib().dcte_set_option(self._h, opt, float(value)))
+
+    def profile_read(self):
+        """-> (map-kernel launches, summed device ms) since the last read."""
+        n = ctypes.c_longlong()
+        ms = ctypes.c_double()
+        self._check(lib().dcte_profile_read(self._h, ctypes.byref(n), ctypes.byref(ms)))
+        return n.value, ms.value
+
+    # -- host entry point
+    def energy_map(self, px, n=8, edges=0.5, textures=0.5, semantics=DCTE_LQR,
+                   transposed=False, out=None):
+        """Energy map of an HxW (grey) or HxWxC uint8 frame -> HxW float32."""
+        px = np.asarray(px)
+        if px.dtype != np.uint8:
+            raise TypeError("px must be uint8")
+        if px.ndim == 2:
+            h, w = px.shape
+            bpp = 1
+        elif px.ndim == 3:
+            h, w, bpp = px.shape
+        else:
+            raise ValueError("px must be HxW or HxWxC")
+        if px.strides[-1] != 1 or (px.ndim == 3 and px.strides[1] != bpp):
+            px = np.ascontiguousarray(px)
+        rowstride = px.strides[0]
+        if out is None:
+            out = np.empty((h, w), np.float32)
+        elif out.shape != (h, w) or out.dtype != np.float32 or not out.flags.c_contiguous:
+            raise ValueError("out must be a C-contiguous HxW float32 array")
+        self._check(lib().dcte_energy_map(self._h, px.ctypes.data, w, h, bpp, rowstride, n,
+                                          edges, textures, semantics, int(bool(transposed)),
+                                          out.ctypes.data))
+        return out
+
+    # -- device entry point (HBM-resident frames; addresses as ints)
+    def energy_map_device(self, d_px, rowstride, w, h, bpp, in_row0, in_rows, y0, y1, n,
+                          edges, textures, d_out, out_stride, stream=0, device=0):
+        self._check(lib().dcte_energy_map_device(
+            self._h, device, ctypes.c_void_p(d_px), rowstride, w, h, bpp, in_row0, in_rows,
+            y0, y1, n, edges, textures, ctypes.c_void_p(d_out), out_stride,
+            ctypes.c_void_p(stream)))
+
+    def energy_map_tensor(self, px, out, n=8, edges=0.5, textures=0.5, h=None, in_row0=0,
+                          y0=None, y1=None, stream=None, device=0):
+        """torch.uint8 CUDA frame rows (HxW or HxWxC; row 0 = global row
+        `in_row0` of an image of height `h`) -> rows [y0, y1) into `out`."""
+        import torch  # plumbing only: device memory and the current stream
+        if px.device.type != "cuda" or out.device.type != "cuda":
+            raise ValueError("tensors must live on a HIP device")
+        if px.dtype != torch.uint8 or out.dtype != torch.float32:
+            raise TypeError("px uint8, out float32")
+        rows, w = px.shape[0], px.shape[1]
+        bpp = 1 if px.dim() == 2 else px.shape[2]
+        if px.stride(-1) != 1 or (px.dim() == 3 and px.stride(1) != bpp):
+            raise ValueError("px rows must be dense")
+        if out.stride(-1) != 1:
+            raise ValueError("out rows must be dense")
+        h = rows if h is None else h
+        y0 = in_row0 if y0 is None else y0
+        y1 = in_row0 + rows if y1 is None else y1
+        if stream is None:
+            stream = torch.cuda.current_stream(px.device).cuda_stream
+        self.energy_map_device(px.data_ptr(), px.stride(0), w, h, bpp, in_row0, rows, y0, y1,
+                               n, edges, textures, out.data_ptr(), out.stride(0), stream, device)
+        return out
+
+
+__all__ = ["Context", "DcteError", "lib", "device_count", "LIB_PATH", "EXPORTS",
+           "DCTE_LQR", "DCTE_PREVIEW", "DCTE_OPT_TIE_TAU", "DCTE_OPT_PROFILE"]

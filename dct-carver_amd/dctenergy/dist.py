@@ -1,0 +1,106 @@
+"""Row-band sharding of one frame over ranks (one process per GPU).
+
+Rank k of G owns global rows [Y0, Y1) of a frame of height H.  An output row
+y reads input rows y-(N/2-1) .. y+N/2 (src/render.c:146-152; replicate clamp
+at the *global* image border), so a band needs hl = N/2-1 rows from the rank
+above (its top halo) and hr = N/2 rows from the rank below (its bottom halo).
+Those rows are the only bytes that cross ranks: one point-to-point exchange
+per frame (RCCL over xGMI with backend "nccl"; gloo on CPU in tests).
+
+The band buffer holds [top halo | own rows | bottom halo] contiguously, so the
+kernel addresses it as global rows [Y0 - top, Y1 + bot).
+"""
+from dataclasses import dataclass
+
+
+@dataclass(frozen=True)
+class Band:
+    rank: int
+    world: int
+    H: int          # global frame height
+    Y0: int         # own rows [Y0, Y1)
+    Y1: int
+    hl: int         # N/2 - 1
+    hr: int         # N/2
+
+    @property
+    def own(self):
+        return self.Y1 - self.Y0
+
+    @property
+    def top(self):
+        """halo rows held above Y0 (none at the global top)"""
+        return self.hl if self.rank > 0 else 0
+
+    @property
+    def bot(self):
+        """halo rows held below Y1 (none at the global bottom)"""
+        return self.hr if self.rank < self.world - 1 else 0
+
+    @property
+    def rows(self):
+        return self.top + self.own + self.bot
+
+    @property
+    def row0(self):
+        """global row index of buffer row 0"""
+        return self.Y0 - self.top
+
+    def interior(self):
+        """output rows computable from own rows alone (before the halos land)"""
+        return self.Y0 + self.top, self.Y1 - self.bot
+
+    def edges(self):
+        """output row ranges that need a halo"""
+        out = []
+        if self.top:
+            out.append((self.Y0, self.Y0 + self.top))
+        if self.bot:
+            out.append((self.Y1 - self.bot, self.Y1))
+        return out
+
+
+def make_band(H, rank, world, n, rows_per_rank=None):
+    """Band of `rank`.  rows_per_rank=None splits H evenly (strong scaling);
+    otherwise every rank owns rows_per_rank rows of a frame of height
+    world * rows_per_rank (weak scaling)."""
+    if rows_per_rank is None:
+        Y0, Y1 = H * rank // world, H * (rank + 1) // world
+    else:
+        if H != world * rows_per_rank:
+            raise ValueError("weak scaling: H must be world * rows_per_rank")
+        Y0, Y1 = rank * rows_per_rank, (rank + 1) * rows_per_rank
+    band = Band(rank, world, H, Y0, Y1, n // 2 - 1, n // 2)
+    if world > 1 and band.own < band.hr:
+        raise ValueError(f"every rank needs >= {band.hr} rows (N={n})")
+    return band
+
+
+def halo_ops(buf, band, group=None):
+    """P2P ops that fill `buf`'s halo rows from the neighbour ranks and send
+    this rank's edge rows to them (buf: [band.rows, ...] contiguous tensor).
+
+    rank k-1's bottom halo = my first hr own rows; rank k+1's top halo = my
+    last hl own rows."""
+    import torch.distributed as dist
+    ops = []
+    k, G = band.rank, band.world
+    t, own = band.top, band.own
+    if k > 0:
+        if band.hl:
+            ops.append(dist.P2POp(dist.irecv, buf[:t], k - 1, group))
+        ops.append(dist.P2POp(dist.isend, buf[t:t + band.hr], k - 1, group))
+    if k < G - 1:
+        ops.append(dist.P2POp(dist.irecv, buf[t + own:], k + 1, group))
+        if band.hl:
+            ops.append(dist.P2POp(dist.isend, buf[t + own - band.hl:t + own], k + 1, group))
+    return ops
+
+
+def exchange_halos(buf, band, group=None):
+    """Start the halo exchange; returns the request list (empty at world 1)."""
+    import torch.distributed as dist
+    ops = halo_ops(buf, band, group)
+    if not ops:
+        return []
+    return dist.batch_isend_irecv(ops)

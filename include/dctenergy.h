@@ -1,0 +1,132 @@
+/*
+ * dctenergy.h -- C ABI of libdctenergy_hip.so, the MI355X (gfx950) backend
+ * for the dct-carver energy map.
+ *
+ * Plain C types only (no HIP, GIMP, glib or liblqr types), so the existing C
+ * plug-in links it without new build dependencies.
+ *
+ * What it replaces, in the reference (avivrosenberg/dct-carver):
+ *   - the per-pixel liblqr energy callback dct_pixel_energy
+ *     (src/render.c:134-157, registered at src/render.c:314-315 with radius
+ *     N/2 and LQR_ER_LUMA), called W*H times by liblqr's energy build, and
+ *     the arithmetic under it: dctNxN (src/dct.c:93-110) ->
+ *     ddct8x8s / ddct16x16s / ddct2d (src/fft2d/shrtdct.c:55, :231;
+ *     src/fft2d/fftsg2d.c:566) and weighted_max_dct_correlation
+ *     (src/dct.c:112-126).  dcte_energy_map computes all W*H callback
+ *     results of one carver build in one call; the plug-in then serves
+ *     dct_pixel_energy(x, y, ...) from the returned map.
+ *
+ * Semantics (DCTE_LQR): out[y*w + x] = the value dct_pixel_energy(x, y, w, h,
+ * rw, params) returns for a carver built on these pixels with blocksize N,
+ * edges, textures -- liblqr luma 0.2126 R + 0.7152 G + 0.0722 B on channel/255
+ * (grey: v/255) [liblqr, unverified], window offsets -(N/2-1)..N/2 with
+ * replicate clamp, 2-D DCT-II (orthonormal N=8,16; unnormalised N=2,4),
+ * weighted max with the last-maximum tie rule.  Results agree with the
+ * reference CPU path to <= 1e-5 relative (measured ~3e-7), bit-exactly
+ * wherever the edge/texture decision is within the fp32 error band.
+ *
+ * Errors: every entry point returns DCTE_OK (0) or a negative DCTE_E* code
+ * and never exits the process (the reference exit(1)s on OOM,
+ * src/fft2d/alloc.c:5-10, and silently leaves the data untransformed for a
+ * bad N, src/dct.c:105-108; here a bad N is DCTE_EINVAL).
+ *
+ * Threading: one context serves one thread at a time (the reference callback
+ * is not re-entrant either: it shares params->data, src/render.c:140).
+ */
+#ifndef DCTENERGY_H
+#define DCTENERGY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DCTE_ABI_VERSION 1
+
+/* status codes */
+#define DCTE_OK 0
+#define DCTE_EINVAL (-1)   /* bad argument (N not in {2,4,8,16}, sizes, bpp) */
+#define DCTE_ENODEV (-2)   /* no usable gfx950 device */
+#define DCTE_ENOMEM (-3)   /* device or host allocation failed */
+#define DCTE_EHIP (-4)     /* HIP runtime error (see dcte_last_error) */
+#define DCTE_ERANGE (-5)   /* frame too large for one launch (> 4 GiB band) */
+#define DCTE_ENOTSUP (-6)  /* recognised but not provided by this build */
+
+/* energy semantics */
+#define DCTE_LQR 0         /* liblqr callback semantics, src/render.c:134-157 */
+#define DCTE_PREVIEW 1     /* GTK preview semantics, src/render.c:31-109 */
+
+/* options for dcte_set_option */
+#define DCTE_OPT_TIE_TAU 1 /* relative edge/texture margin refined in fp64
+                              (default 4e-6; 0 = never refine, >= 1 = refine
+                              every pixel) */
+#define DCTE_OPT_PROFILE 2 /* 1 = bracket every map-kernel launch with HIP
+                              events on its stream (dcte_profile_read) */
+
+typedef struct dcte_ctx dcte_ctx;
+
+int dcte_abi_version(void);
+
+/* Number of visible HIP devices (0 when none; never an error). */
+int dcte_device_count(void);
+
+/* Create a context on `ngpus` devices (0 = all visible).  Device memory,
+ * streams and kernels are set up lazily on first use.  flags: reserved, 0. */
+int dcte_create(dcte_ctx **ctx, int ngpus, unsigned flags);
+void dcte_destroy(dcte_ctx *ctx);
+
+/* Number of devices the context uses. */
+int dcte_ctx_devices(const dcte_ctx *ctx);
+
+int dcte_set_option(dcte_ctx *ctx, int option, double value);
+
+/* Host-buffer entry point: the full energy map of one frame.
+ *   px        8-bit interleaved pixels, bpp channels (1 grey, 3 RGB), row y
+ *             at px + y*rowstride (the buffer the plug-in hands to
+ *             lqr_carver_new, src/render.c:159-173,312)
+ *   n         blocksize N (2, 4, 8, 16)
+ *   edges, textures   weights (PlugInVals, src/main.h:12-22)
+ *   semantics DCTE_LQR
+ *   transposed 0 (1 = map of the transposed frame; not in this build)
+ *   out       caller-owned w*h floats, row-major
+ * With several devices the frame is split into row bands; each device
+ * receives its band plus the N/2-row halo straight from `px`. */
+int dcte_energy_map(dcte_ctx *ctx, const uint8_t *px, int w, int h, int bpp,
+                    size_t rowstride, int n, float edges, float textures,
+                    int semantics, int transposed, float *out);
+
+/* Device-resident entry point (frames already in HBM; no copies, no sync).
+ *   device    index into the context's devices
+ *   d_px      device pointer to global row in_row0 of a w x h frame; rows
+ *             [in_row0, in_row0 + in_rows) are readable and must include
+ *             every row the clamp reaches for [y0, y1)
+ *   d_out     device pointer; row y (y0 <= y < y1) at d_out + (y-y0)*out_stride
+ *   stream    hipStream_t (NULL = default stream) the work is ordered on
+ * Calls on different streams may run concurrently (separate scratch). */
+int dcte_energy_map_device(dcte_ctx *ctx, int device, const void *d_px,
+                           long long rowstride, int w, int h, int bpp,
+                           int in_row0, int in_rows, int y0, int y1, int n,
+                           float edges, float textures, float *d_out,
+                           long long out_stride, void *stream);
+
+/* Pixels recomputed by the fp64 refinement in the last dcte_energy_map call
+ * (diagnostic; device calls are not synchronised, so not counted). */
+long long dcte_last_refined(const dcte_ctx *ctx);
+
+/* Profiling (DCTE_OPT_PROFILE = 1): synchronises the recorded events and
+ * returns the number of map-kernel launches and their summed device time
+ * since the last read, then resets. */
+int dcte_profile_read(dcte_ctx *ctx, long long *launches, double *kernel_ms);
+
+const char *dcte_strerror(int code);
+
+/* Text of the last HIP error seen by this context ("" if none). */
+const char *dcte_last_error(const dcte_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DCTENERGY_H */

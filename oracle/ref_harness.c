@@ -1,0 +1,144 @@
+/*
+ * ref_harness.c -- drives the REFERENCE's own compiled transforms.
+ *
+ * TEST INFRASTRUCTURE ONLY (see dcte_oracle.c).  Built by oracle/Makefile
+ * into oracle/_ref/libdcte_ref.so together with the reference's unmodified
+ * src/fft2d/{alloc,fftsg,fftsg2d,shrtdct}.c, compiled where they lie under
+ * /root/reference with the reference's own flags (-DUSE_FFT2D_PTHREADS,
+ * src/fft2d/Makefile.am:13-16).
+ *
+ * src/dct.c and src/render.c cannot be compiled here (they need the GIMP,
+ * GTK and liblqr headers, which this image lacks), so the two thin pieces of
+ * glue around the transforms are restated below, with the reference's own
+ * scratch layout (row-pointer arrays from alloc_2d_double, ip[] / w[] sized
+ * as in src/render.c:302-305, ip[0] = 0 once per carver):
+ *   - dctNxN dispatch           src/dct.c:93-110
+ *   - weighted max + edge LUT   src/dct.c:72-89, 112-126
+ *   - window gather + clamp     src/render.c:122-157
+ * Everything numeric (ddct8x8s, ddct16x16s, ddct2d) is the reference's code.
+ */
+#include <math.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+/* prototypes as declared by the reference at src/dct.c:67-69 */
+void ddct8x8s(int isgn, double **a);
+void ddct16x16s(int isgn, double **a);
+void ddct2d(int n1, int n2, int isgn, double **a, double *t, int *ip, double *w);
+/* from src/fft2d/alloc.h */
+int *alloc_1d_int(int n1);
+void free_1d_int(int *i);
+double *alloc_1d_double(int n1);
+void free_1d_double(double *d);
+double **alloc_2d_double(int n1, int n2);
+void free_2d_double(double **dd);
+
+typedef struct {
+    int n;
+    int *ip;
+    double *w;
+    double **data;
+} ref_scratch;
+
+static void scratch_init(ref_scratch *s, int n)
+{
+    s->n = n;
+    s->ip = alloc_1d_int(2 + (int)sqrt(n / 2 + 0.5));
+    s->w = alloc_1d_double(n * 3 / 2);
+    s->data = alloc_2d_double(n, n);
+    s->ip[0] = 0;
+}
+
+static void scratch_free(ref_scratch *s)
+{
+    free_1d_int(s->ip);
+    free_1d_double(s->w);
+    free_2d_double(s->data);
+}
+
+static void dispatch(ref_scratch *s)
+{
+    switch (s->n) {
+    case 2:
+    case 4: ddct2d(s->n, s->n, -1, s->data, NULL, s->ip, s->w); break;
+    case 8: ddct8x8s(-1, s->data); break;
+    case 16: ddct16x16s(-1, s->data); break;
+    default: break;
+    }
+}
+
+static float weighted_max(const ref_scratch *s, float edges, float textures)
+{
+    int k1, k2, b1 = 0, b2 = 0, n = s->n;
+    double m = 0, v;
+    for (k1 = 0; k1 < n; k1++)
+        for (k2 = 0; k2 < n; k2++) {
+            v = fabs(s->data[k1][k2]);
+            if (m <= v && (k1 || k2)) {
+                m = v;
+                b1 = k1;
+                b2 = k2;
+            }
+        }
+    int edge = (b1 == 0 && b2 == 1) || (b1 == 1 && b2 == 0);
+    return edge ? (float)(m * edges) : (float)(m * textures);
+}
+
+static int clamp_off(int base, int off, int lo, int hi)
+{
+    if (base + off - lo < 0) return off - (base + off - lo);
+    if (base + off - hi > 0) return off - (base + off - hi);
+    return off;
+}
+
+/* In-place reference transform of an n*n window given as a flat [dx][dy] array. */
+int ref_dct(int n, double *win)
+{
+    ref_scratch s;
+    if (n != 2 && n != 4 && n != 8 && n != 16) return -1;
+    scratch_init(&s, n);
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) s.data[i][j] = win[i * n + j];
+    dispatch(&s);
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) win[i * n + j] = s.data[i][j];
+    scratch_free(&s);
+    return 0;
+}
+
+float ref_window_energy(int n, const double *win, float edges, float textures)
+{
+    ref_scratch s;
+    scratch_init(&s, n);
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) s.data[i][j] = win[i * n + j];
+    dispatch(&s);
+    float e = weighted_max(&s, edges, textures);
+    scratch_free(&s);
+    return e;
+}
+
+/* Full map over a w*h luma plane (row-major doubles), serial, in liblqr's
+ * build order (rows outer, columns inner), one scratch per "carver". */
+int ref_energy_map_luma(const double *luma, int w, int h, int n, float edges,
+                        float textures, float *out)
+{
+    if (n != 2 && n != 4 && n != 8 && n != 16) return -1;
+    ref_scratch s;
+    scratch_init(&s, n);
+    int r = n / 2;
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            for (int i = -r + 1; i <= r; i++)
+                for (int j = -r + 1; j <= r; j++) {
+                    int ii = clamp_off(x, i, 0, w - 1);
+                    int jj = clamp_off(y, j, 0, h - 1);
+                    s.data[i + r - 1][j + r - 1] = luma[(size_t)(y + jj) * w + (x + ii)];
+                }
+            dispatch(&s);
+            out[(size_t)y * w + x] = weighted_max(&s, edges, textures);
+        }
+    scratch_free(&s);
+    return 0;
+}

@@ -1,0 +1,75 @@
+// dcte_emu.cpp -- host emulation of the gfx950 kernel's fp32 arithmetic.
+//
+// TEST INFRASTRUCTURE.  Runs dcte_passes.h / dcte_math.h (the kernel's own
+// code) on the CPU, pixel by pixel, so CPU-only tests can measure the fp32
+// path's error against the oracle on large and adversarial inputs, and GPU
+// tests can demand bit-equality between device and emulation.
+#include <math.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "dcte_luma.h"
+#include "dcte_passes.h"
+
+using namespace dcte;
+
+namespace {
+
+inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+inline float luma_biased(const uint8_t* p, int bpp)
+{
+    int L = bpp == 1 ? kLumaGrey * (int)p[0]
+                     : kLumaR * (int)p[0] + kLumaG * (int)p[1] + kLumaB * (int)p[2];
+    return (float)(L - kLumaBias);
+}
+
+template <int N>
+void pixel(const uint8_t* px, int w, int h, int bpp, size_t rs, int x, int y, float& mt, float& me)
+{
+    constexpr int CH = Lanes<N>::CH, S = Lanes<N>::S;
+    float lrow[N];
+    float ring[N][CH];
+    float mts[2] = {0, 0}, mes[2] = {0, 0};
+    for (int lp = 0; lp < S; lp++) {
+        for (int j = 0; j < N; j++) {   // input row y - (N/2 - 1) + j -> slot j
+            int t = clampi(y - (N / 2 - 1) + j, 0, h - 1);
+            for (int i = 0; i < N; i++) {
+                int xx = clampi(x - (N / 2 - 1) + i, 0, w - 1);
+                lrow[i] = luma_biased(px + (size_t)t * rs + (size_t)xx * bpp, bpp);
+            }
+            row_pass<N>(lrow, 0, lp, ring[j]);
+        }
+        Cols<N>::template run<0>(ring, lp, mts[lp], mes[lp]);
+    }
+    mt = fmaxf(mts[0], mts[1]);
+    me = fmaxf(mes[0], mes[1]);
+}
+
+}  // namespace
+
+extern "C" {
+
+// Per-pixel emulation over rows [y0, y1).  we / wt are the kernel's scaled
+// weights; outputs E (the kernel's fast-path value), and the raw m_e / m_t.
+int emu_energy_map(const uint8_t* px, int w, int h, int bpp, size_t rowstride, int n,
+                   float we, float wt, int y0, int y1, float* E, float* me_out, float* mt_out)
+{
+    for (int y = y0; y < y1; y++)
+        for (int x = 0; x < w; x++) {
+            float mt, me;
+            switch (n) {
+            case 2: pixel<2>(px, w, h, bpp, rowstride, x, y, mt, me); break;
+            case 4: pixel<4>(px, w, h, bpp, rowstride, x, y, mt, me); break;
+            case 8: pixel<8>(px, w, h, bpp, rowstride, x, y, mt, me); break;
+            case 16: pixel<16>(px, w, h, bpp, rowstride, x, y, mt, me); break;
+            default: return -1;
+            }
+            size_t k = (size_t)(y - y0) * w + x;
+            E[k] = me > mt ? me * we : mt * wt;
+            if (me_out) me_out[k] = me;
+            if (mt_out) mt_out[k] = mt;
+        }
+    return 0;
+}
+}

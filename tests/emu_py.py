@@ -1,0 +1,64 @@
+"""ctypes view of tests/emu (host emulation of the kernels' fp32 arithmetic)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+EMU_DIR = os.path.join(HERE, "emu")
+EMU_SO = os.path.join(EMU_DIR, "build", "libdcte_emu.so")
+LUMA_SCALE = 1275000.0
+TIE_TAU = 4e-6   # kDefaultTieTau in dcte_capi.cpp
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_f32p = ctypes.POINTER(ctypes.c_float)
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        subprocess.run(["make", "-s", "-C", EMU_DIR], check=True)
+        L = ctypes.CDLL(EMU_SO)
+        L.emu_energy_map.restype = ctypes.c_int
+        L.emu_energy_map.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_size_t, ctypes.c_int, ctypes.c_float,
+                                     ctypes.c_float, ctypes.c_int, ctypes.c_int,
+                                     _f32p, _f32p, _f32p]
+        _lib = L
+    return _lib
+
+
+def scale(n):
+    return LUMA_SCALE * (n if n >= 8 else 1)
+
+
+def kernel_weights(n, edges, textures):
+    """The launcher's pre-scaled weights (dcte_capi.cpp run_device)."""
+    s = scale(n)
+    return np.float32(np.float64(np.float32(edges)) / s), np.float32(np.float64(np.float32(textures)) / s)
+
+
+def energy_map(img, n, edges, textures):
+    """-> (E_fast, m_e, m_t), exactly the kernel's fast-path values."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape[:2]
+    bpp = 1 if img.ndim == 2 else img.shape[2]
+    we, wt = kernel_weights(n, edges, textures)
+    E = np.empty((h, w), np.float32)
+    me = np.empty_like(E)
+    mt = np.empty_like(E)
+    rc = lib().emu_energy_map(img.ctypes.data_as(_u8p), w, h, bpp, w * bpp, n, we, wt, 0, h,
+                              E.ctypes.data_as(_f32p), me.ctypes.data_as(_f32p),
+                              mt.ctypes.data_as(_f32p))
+    assert rc == 0
+    return E, me, mt
+
+
+def refine_mask(me, mt, edges, textures, tau=TIE_TAU):
+    """Pixels the kernel hands to the fp64 refinement (same predicate)."""
+    if np.float32(edges) == np.float32(textures):
+        return np.zeros(me.shape, bool)
+    hi = np.maximum(me, mt)
+    return (hi > 0) & (np.abs(me - mt) <= np.float32(tau) * hi)
