@@ -98,6 +98,7 @@ __global__ __launch_bounds__(kThreads) void dcte_map(const MapParams p)
     const uint32_t base_off = (uint32_t)(pbase & 3u);
     const unsigned nrec = base_off + (unsigned)((long long)(p.in_rows - 1) * p.rowstride) +
                           (unsigned)(w * BPP);
+    const unsigned nrec4 = nrec & ~3u;                // bytes covered by whole dwords
     __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<void*>(pbase - base_off), (short)0, (int)nrec, (int)kBufFlags);
 
@@ -106,6 +107,18 @@ __global__ __launch_bounds__(kThreads) void dcte_map(const MapParams p)
         return base_off + (uint32_t)((long long)(t - p.in_row0) * p.rowstride) +
                (uint32_t)(xs * BPP);
     };
+
+    // A dword straddling the end of the readable bytes reads as 0 (buffer
+    // bounds are checked per dword).  The workgroups whose span reaches the
+    // last readable row's last pixel fetch those <= 3 tail bytes once here and
+    // patch them in when staging raw rows.
+    const bool tail_wg = (nrec & 3u) != 0u && x0 + TW + Gm::HR - 1 >= w - 1 &&
+                         min(h - 1, ye - 1 + Gm::HR) >= p.in_row0 + p.in_rows - 1;
+    uint32_t tail = 0;
+    if (tail_wg) {
+        for (uint32_t b = 0; b < (nrec & 3u); b++)
+            tail |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, (int)(nrec4 + b), 0, 0) << (8u * b);
+    }
 
     uint32_t pref[G];
     auto issue = [&](int g) {
@@ -125,7 +138,15 @@ __global__ __launch_bounds__(kThreads) void dcte_map(const MapParams p)
         // stage raw bytes of group g, then prefetch group g + 1
         if (tx < NDW) {
 #pragma unroll
-            for (int u = 0; u < G; u++) raw[u][tx] = pref[u];
+            for (int u = 0; u < G; u++) {
+                uint32_t v = pref[u];
+                if (tail_wg) {                     // uniform; a handful of WGs
+                    int i = g * G + u;
+                    uint32_t a = (row_start(i < n_in ? i : n_in - 1) & ~3u) + 4u * tx;
+                    if (a == nrec4) v = tail;
+                }
+                raw[u][tx] = v;
+            }
         }
         if (g + 1 < ngroups) issue(g + 1);
         __syncthreads();
@@ -137,11 +158,16 @@ __global__ __launch_bounds__(kThreads) void dcte_map(const MapParams p)
                 uint32_t rs = row_start(g * G + u);
                 uint32_t off = (rs & 3u) + (uint32_t)((xc - xs) * BPP);
                 const uint8_t* rb = reinterpret_cast<const uint8_t*>(&raw[u][0]);
+                uint32_t c0 = rb[off], c1 = 0, c2 = 0;
+                if constexpr (BPP == 3) {
+                    c1 = rb[off + 1];
+                    c2 = rb[off + 2];
+                }
                 int L;
                 if constexpr (BPP == 1) {
-                    L = kLumaGrey * (int)rb[off];
+                    L = kLumaGrey * (int)c0;
                 } else {
-                    L = kLumaR * (int)rb[off] + kLumaG * (int)rb[off + 1] + kLumaB * (int)rb[off + 2];
+                    L = kLumaR * (int)c0 + kLumaG * (int)c1 + kLumaB * (int)c2;
                 }
                 lum[u][cc] = (float)(L - kLumaBias);
             }

@@ -1,0 +1,48 @@
+/*
+ * dcte_plugin.h -- plug-in side glue for libdctenergy_hip.so.
+ *
+ * Compiled INTO the dct-carver plug-in (plain C, no GIMP/liblqr types), next
+ * to src/render.c.  The plug-in keeps one dcte_map_cache in its
+ * EnergyParameters (src/render.h:9-16), fills it once per carver in
+ * init_carver_from_vals (src/render.c:286-325) and lets dct_pixel_energy
+ * (src/render.c:134-157) answer from it while liblqr asks for pixels of the
+ * frame the map was built on (same width/height, horizontal orientation).
+ * Every other call -- after a seam changed the carver size, in the
+ * transposed (vertical) orientation, or when no GPU is present -- runs the
+ * plug-in's original per-window code unchanged.  INTEGRATION.md has the patch.
+ */
+#ifndef DCTE_PLUGIN_H
+#define DCTE_PLUGIN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+    float *map;      /* w*h energies, row-major, owned */
+    int w, h;
+    int valid;
+    int status;      /* DCTE_* code of the last build */
+} dcte_map_cache;
+
+/* Build the map for the frame handed to lqr_carver_new (src/render.c:312).
+ * Returns DCTE_OK, or an error code after which the cache stays invalid
+ * and every lookup misses (the plug-in then runs its original code). */
+int dcte_plugin_build(dcte_map_cache *c, const uint8_t *px, int w, int h, int bpp,
+                      size_t rowstride, int blocksize, float edges, float textures);
+
+/* 1 and *out = energy when (x, y) of a w x h carver in orientation 0 is
+ * served from the map; 0 otherwise. */
+int dcte_plugin_lookup(const dcte_map_cache *c, int x, int y, int w, int h,
+                       int orientation, float *out);
+
+void dcte_plugin_release(dcte_map_cache *c);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DCTE_PLUGIN_H */
