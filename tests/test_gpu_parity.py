@@ -207,4 +207,9 @@ def test_ties_are_refined_to_reference(ctx):
             ref = O.energy_map(img, n, 0.3, 0.7)
             got = ctx.energy_map(img, n, 0.3, 0.7)
             _assert_tol(got, ref, f"ties n={n}")
-            assert ctx.last_refined > 0
+            # the device flags exactly the pixels the emulated fp32 path puts
+            # inside the refinement band
+            _, me, mt = EM.energy_map(img, n, 0.3, 0.7)
+            assert ctx.last_refined == int(EM.refine_mask(me, mt, 0.3, 0.7).sum())
+            if n < 16:
+                assert ctx.last_refined > 0

@@ -1,0 +1,80 @@
+"""Summarise rocprofv3 runs of bench.py into profiles/pmc_summary.json and copy
+the raw summaries into profiles/<round>/.
+
+    python tools/pmc_summary.py gpurun_out r01 [--size 16384] [--n 8]
+
+Counter corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE is in KiB and on
+gfx950 counts 128-B fabric reads as 64 B, so HBM read bytes = 2 x FETCH_SIZE x
+1024; WRITE_SIZE (KiB) is exact.  SQ_INSTS_VALU counts wave64 instructions
+(lane-ops = x 64).  Effective clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel time.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_dispatch(path, kernel_substr):
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    for r in csv.DictReader(open(path)):
+        if kernel_substr not in r["Kernel_Name"]:
+            continue
+        agg[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    return {k: sum(v.values()) / len(v) for k, v in agg.items() if v}
+
+
+def main():
+    src, rnd = sys.argv[1], sys.argv[2]
+    size = int(sys.argv[sys.argv.index("--size") + 1]) if "--size" in sys.argv else 16384
+    n = int(sys.argv[sys.argv.index("--n") + 1]) if "--n" in sys.argv else 8
+    kname = f"dcte_map<{n}, 3>"
+    dst = os.path.join(ROOT, "profiles", rnd)
+    os.makedirs(dst, exist_ok=True)
+    counters = {}
+    for f in glob.glob(os.path.join(src, "pmc_*", "*counter_collection.csv")):
+        counters.update(per_dispatch(f, kname))
+        tag = os.path.basename(os.path.dirname(f))
+        shutil.copy(f, os.path.join(dst, f"{tag}.csv"))
+    stats = os.path.join(src, "prof_trace", "run_kernel_stats.csv")
+    kern_ns = None
+    if os.path.exists(stats):
+        shutil.copy(stats, os.path.join(dst, "kernel_stats.csv"))
+        for r in csv.DictReader(open(stats)):
+            if kname in r["Name"]:
+                kern_ns = float(r["AverageNs"])
+    px = size * size
+    out = {"kernel": kname, "frame": [size, size], "pixels": px,
+           "kernel_avg_ns_traced": kern_ns, "raw_counters_per_dispatch": counters}
+    if "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
+        rd = 2 * counters["FETCH_SIZE"] * 1024
+        wr = counters["WRITE_SIZE"] * 1024
+        out["hbm_read_bytes_per_launch"] = rd
+        out["hbm_write_bytes_per_launch"] = wr
+        out["hbm_bytes_per_launch"] = rd + wr
+        out["algorithmic_bytes_per_launch"] = px * 7
+    if "SQ_INSTS_VALU" in counters:
+        out["valu_lane_ops_per_px"] = round(counters["SQ_INSTS_VALU"] * 64 / px, 2)
+    if "GRBM_GUI_ACTIVE" in counters and kern_ns:
+        out["effective_clock_ghz"] = round(counters["GRBM_GUI_ACTIVE"] / 8 / kern_ns, 3)
+    if "SQ_INSTS_VALU" in counters and "GRBM_GUI_ACTIVE" in counters:
+        cyc = counters["GRBM_GUI_ACTIVE"] / 8
+        out["valu_issue_utilisation"] = round(counters["SQ_INSTS_VALU"] / (1024 * cyc / 2), 4)
+    if "SQ_WAVE_CYCLES" in counters:
+        for k in ("SQ_WAIT_INST_ANY", "SQ_WAIT_ANY"):
+            if k in counters:
+                out[k.lower() + "_frac"] = round(counters[k] / counters["SQ_WAVE_CYCLES"], 4)
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    allsum = json.load(open(path)) if os.path.exists(path) else {}
+    allsum[f"dcte_map<{n},3>@{size}"] = dict(out, round=rnd)
+    json.dump(allsum, open(path, "w"), indent=1)
+    json.dump(out, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
