@@ -38,6 +38,19 @@
 namespace dcte {
 
 constexpr int kThreads = 256;
+// build-time tuning knobs (tools/variants.sh A/Bs them on the GPU)
+#ifndef DCTE_TILE_H
+#define DCTE_TILE_H 128
+#endif
+#ifndef DCTE_TILE_H16
+#define DCTE_TILE_H16 128
+#endif
+#ifndef DCTE_G8
+#define DCTE_G8 8          // rows per staging group for N = 8 (multiple of 8)
+#endif
+#ifndef DCTE_MIN_WAVES
+#define DCTE_MIN_WAVES 1   // __launch_bounds__ minimum waves per SIMD
+#endif
 constexpr unsigned kBufFlags = 0x00020000u;  // gfx9 raw buffer dword3
 
 template <int N>
@@ -49,7 +62,7 @@ struct Geo {
     static constexpr int HR = N / 2;                     // halo right / bottom
     static constexpr int LW = TW + N - 1;                // luma columns per row
     static constexpr int LWP = LW + 1;
-    static constexpr int G = (N < 8) ? 8 : N;            // rows per group (multiple of N)
+    static constexpr int G = (N < 8) ? 8 : (N == 8 ? DCTE_G8 : N);  // rows per group (multiple of N)
     template <int BPP>
     static constexpr int ndw() { return (LW * BPP + 3) / 4 + 1; }  // dwords per raw row
 };
@@ -69,7 +82,7 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? l
 
 // ------------------------------------------------------------------ main kernel
 template <int N, int BPP>
-__global__ __launch_bounds__(kThreads) void dcte_map(const MapParams p)
+__global__ __launch_bounds__(kThreads, DCTE_MIN_WAVES) void dcte_map(const MapParams p)
 {
     using Gm = Geo<N>;
     constexpr int S = Gm::S, CH = Gm::CH, TW = Gm::TW, HL = Gm::HL;
@@ -231,7 +244,7 @@ __global__ __launch_bounds__(64) void dcte_fix(const FixParams p)
 
 // ------------------------------------------------------------------ launchers
 int map_tile_w(int n) { return n == 16 ? Geo<16>::TW : kThreads; }
-int map_default_tile_h(int n) { return n == 16 ? 128 : 128; }
+int map_default_tile_h(int n) { return n == 16 ? DCTE_TILE_H16 : DCTE_TILE_H; }
 
 template <int N, int BPP>
 static hipError_t launch_map_t(const MapParams& p, hipStream_t s)

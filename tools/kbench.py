@@ -1,0 +1,79 @@
+"""Kernel A/B on the GPU: time dcte_map over a 16384^2 RGB frame for several
+builds of libdctenergy_hip.so, interleaved rounds in ONE process per build
+set (cdna_hip_programming.md rule 24).
+
+    python tools/kbench.py --n 8 --size 16384 build/variants/a.so build/variants/b.so ...
+Each .so is loaded under its own ctypes handle; prints one JSON line per build.
+"""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "dct-carver_amd")]
+
+
+def load(path):
+    L = ctypes.CDLL(path)
+    vp = ctypes.c_void_p
+    L.dcte_create.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_uint]
+    L.dcte_set_option.argtypes = [vp, ctypes.c_int, ctypes.c_double]
+    L.dcte_energy_map_device.argtypes = [vp, ctypes.c_int, vp, ctypes.c_longlong, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                         ctypes.c_float, vp, ctypes.c_longlong, vp]
+    L.dcte_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
+    h = vp()
+    assert L.dcte_create(ctypes.byref(h), 1, 0) == 0
+    L.dcte_set_option(h, 2, 1.0)
+    return L, h
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=8)
+    ap.add_argument("--size", type=int, default=16384)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--bpp", type=int, default=3)
+    ap.add_argument("libs", nargs="+")
+    a = ap.parse_args()
+    import torch
+    from dctenergy import synth
+    S = a.size
+    frame = synth.natural_rows(0, S, S, a.bpp, seed=0, device="cuda")
+    out = torch.empty((S, S), dtype=torch.float32, device="cuda")
+    ref = None
+    libs = [(p, *load(p)) for p in a.libs]
+    stream = torch.cuda.current_stream().cuda_stream
+    times = {p: [] for p in a.libs}
+    same = {}
+    for r in range(a.rounds):
+        for p, L, h in libs:
+            for _ in range(a.iters + 1):
+                rc = L.dcte_energy_map_device(h, 0, frame.data_ptr(), frame.stride(0), S, S, a.bpp, 0, S,
+                                              0, S, a.n, 0.3, 0.7, out.data_ptr(), out.stride(0), stream)
+                assert rc == 0, rc
+            n = ctypes.c_longlong()
+            ms = ctypes.c_double()
+            L.dcte_profile_read(h, ctypes.byref(n), ctypes.byref(ms))
+            # drop the first launch of the round (warm)
+            times[p].append(ms.value / n.value)
+            if r == 0:
+                torch.cuda.synchronize()
+                if ref is None:
+                    ref = out.clone()
+                same[p] = bool(torch.equal(out, ref))
+    for p in a.libs:
+        t = times[p]
+        print(json.dumps({"lib": os.path.basename(p), "n": a.n, "size": S,
+                          "median_ms": round(statistics.median(t), 4), "min_ms": round(min(t), 4),
+                          "mpx_s": round(S * S / statistics.median(t) / 1e3, 1),
+                          "bit_equal_first": same[p]}))
+
+
+if __name__ == "__main__":
+    main()
