@@ -19,6 +19,7 @@
 #include "../../include/dctenergy.h"
 #include "dcte_kernels.h"
 #include "dcte_luma.h"
+#include "dcte_norm.h"
 
 namespace {
 
@@ -38,6 +39,10 @@ struct Device {
     float* d_out = nullptr;
     size_t out_cap = 0;
     std::map<hipStream_t, FixScratch> fix;
+    unsigned* d_keys = nullptr;    // min/max scratch (per device; stream-ordered)
+    float* d_minmax = nullptr;
+    uint8_t* d_u8 = nullptr;       // u8 staging for the host entry points
+    size_t u8_cap = 0;
 };
 
 }  // namespace
@@ -193,6 +198,79 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     return DCTE_OK;
 }
 
+int ensure_buf(dcte_ctx* ctx, void** p, size_t* cap, size_t bytes)
+{
+    if (*cap >= bytes) return DCTE_OK;
+    if (*p) DCTE_HIP(ctx, hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    DCTE_HIP(ctx, hipMalloc(p, bytes));
+    *cap = bytes;
+    return DCTE_OK;
+}
+
+int ensure_stream(dcte_ctx* ctx, Device& d)
+{
+    DCTE_HIP(ctx, hipSetDevice(d.id));
+    if (!d.stream) DCTE_HIP(ctx, hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    if (!d.d_keys) {
+        DCTE_HIP(ctx, hipMalloc(&d.d_keys, 2 * sizeof(unsigned) + 2 * sizeof(float)));
+        d.d_minmax = reinterpret_cast<float*>(d.d_keys + 2);
+    }
+    return DCTE_OK;
+}
+
+bool valid_norm(int mode, int channels)
+{
+    return (mode == DCTE_NORM_LQR || mode == DCTE_NORM_PREVIEW) && channels >= 1 && channels <= 4;
+}
+
+// host frame -> device band maps (rows split over the context's devices),
+// left on the devices in d.d_out; returns the number of devices used
+int map_bands(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride, int n,
+              float edges, float textures, int* used)
+{
+    const int G = (int)ctx->devs.size() < h ? (int)ctx->devs.size() : h;
+    const size_t pitch = (size_t)w * bpp;
+    for (int k = 0; k < G; k++) {
+        Device& d = ctx->devs[k];
+        int y0 = (int)((long long)h * k / G), y1 = (int)((long long)h * (k + 1) / G);
+        int lo, hi;
+        needed_rows(n, h, y0, y1, lo, hi);
+        size_t in_bytes = pitch * (size_t)(hi - lo + 1);
+        size_t out_bytes = sizeof(float) * (size_t)w * (size_t)(y1 - y0);
+        int rc = ensure_stream(ctx, d);
+        if (rc) return rc;
+        rc = ensure_buf(ctx, (void**)&d.d_in, &d.in_cap, in_bytes);
+        if (rc) return rc;
+        rc = ensure_buf(ctx, (void**)&d.d_out, &d.out_cap, out_bytes);
+        if (rc) return rc;
+        DCTE_HIP(ctx, hipMemcpy2DAsync(d.d_in, pitch, px + (size_t)lo * rowstride, rowstride,
+                                       pitch, hi - lo + 1, hipMemcpyHostToDevice, d.stream));
+        rc = run_device(ctx, d, d.d_in, (long long)pitch, w, h, bpp, lo, hi - lo + 1, y0, y1, n,
+                        edges, textures, d.d_out, w, d.stream);
+        if (rc) return rc;
+    }
+    *used = G;
+    return DCTE_OK;
+}
+
+int sync_bands(dcte_ctx* ctx, int G)
+{
+    for (int k = 0; k < G; k++) {
+        Device& d = ctx->devs[k];
+        DCTE_HIP(ctx, hipSetDevice(d.id));
+        DCTE_HIP(ctx, hipStreamSynchronize(d.stream));
+        auto it = d.fix.find(d.stream);
+        if (it != d.fix.end()) {
+            unsigned cnt = 0;
+            DCTE_HIP(ctx, hipMemcpy(&cnt, it->second.d_count, sizeof(unsigned), hipMemcpyDeviceToHost));
+            ctx->last_refined += cnt;
+        }
+    }
+    return DCTE_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -238,6 +316,8 @@ void dcte_destroy(dcte_ctx* ctx)
         }
         if (d.d_in) (void)hipFree(d.d_in);
         if (d.d_out) (void)hipFree(d.d_out);
+        if (d.d_keys) (void)hipFree(d.d_keys);
+        if (d.d_u8) (void)hipFree(d.d_u8);
         if (d.stream) (void)hipStreamDestroy(d.stream);
     }
     delete ctx;
@@ -278,52 +358,102 @@ int dcte_energy_map(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, siz
     if (rowstride < (size_t)w * bpp) return DCTE_EINVAL;
     if (semantics != DCTE_LQR) return semantics == DCTE_PREVIEW ? DCTE_ENOTSUP : DCTE_EINVAL;
     if (transposed) return DCTE_ENOTSUP;
-    const int G = (int)ctx->devs.size() < h ? (int)ctx->devs.size() : h;
-    const size_t pitch = (size_t)w * bpp;
     ctx->last_refined = 0;
-    // bands: device k computes rows [k*h/G, (k+1)*h/G) from its band + halo
+    int G = 0;
+    int rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, &G);
+    if (rc) return rc;
     for (int k = 0; k < G; k++) {
         Device& d = ctx->devs[k];
         int y0 = (int)((long long)h * k / G), y1 = (int)((long long)h * (k + 1) / G);
-        int lo, hi;
-        needed_rows(n, h, y0, y1, lo, hi);
-        size_t in_bytes = pitch * (size_t)(hi - lo + 1);
-        size_t out_bytes = sizeof(float) * (size_t)w * (size_t)(y1 - y0);
         DCTE_HIP(ctx, hipSetDevice(d.id));
-        if (!d.stream) DCTE_HIP(ctx, hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-        if (d.in_cap < in_bytes) {
-            if (d.d_in) DCTE_HIP(ctx, hipFree(d.d_in));
-            d.d_in = nullptr;
-            d.in_cap = 0;
-            DCTE_HIP(ctx, hipMalloc(&d.d_in, in_bytes));
-            d.in_cap = in_bytes;
-        }
-        if (d.out_cap < out_bytes) {
-            if (d.d_out) DCTE_HIP(ctx, hipFree(d.d_out));
-            d.d_out = nullptr;
-            d.out_cap = 0;
-            DCTE_HIP(ctx, hipMalloc(&d.d_out, out_bytes));
-            d.out_cap = out_bytes;
-        }
-        DCTE_HIP(ctx, hipMemcpy2DAsync(d.d_in, pitch, px + (size_t)lo * rowstride, rowstride,
-                                       pitch, hi - lo + 1, hipMemcpyHostToDevice, d.stream));
-        int rc = run_device(ctx, d, d.d_in, (long long)pitch, w, h, bpp, lo, hi - lo + 1, y0, y1,
-                            n, edges, textures, d.d_out, w, d.stream);
-        if (rc) return rc;
-        DCTE_HIP(ctx, hipMemcpyAsync(out + (size_t)y0 * w, d.d_out, out_bytes,
+        DCTE_HIP(ctx, hipMemcpyAsync(out + (size_t)y0 * w, d.d_out,
+                                     sizeof(float) * (size_t)w * (size_t)(y1 - y0),
                                      hipMemcpyDeviceToHost, d.stream));
+    }
+    return sync_bands(ctx, G);
+}
+
+int dcte_energy_image_u8(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp,
+                         size_t rowstride, int n, float edges, float textures, int mode,
+                         int channels, uint8_t* out)
+{
+    if (!ctx || !px || !out) return DCTE_EINVAL;
+    if (!valid_n(n) || (bpp != 1 && bpp != 3) || w <= 0 || h <= 0) return DCTE_EINVAL;
+    if (rowstride < (size_t)w * bpp || !valid_norm(mode, channels)) return DCTE_EINVAL;
+    ctx->last_refined = 0;
+    int G = 0;
+    int rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, &G);
+    if (rc) return rc;
+    // per-band min/max, reduced on the host (2 floats per device)
+    float gmin = 0, gmax = 0;
+    for (int k = 0; k < G; k++) {
+        Device& d = ctx->devs[k];
+        int y0 = (int)((long long)h * k / G), y1 = (int)((long long)h * (k + 1) / G);
+        DCTE_HIP(ctx, hipSetDevice(d.id));
+        DCTE_HIP(ctx, dcte::launch_minmax(d.d_out, (long long)w * (y1 - y0), d.d_keys, d.d_minmax, d.stream));
+        float mm[2];
+        DCTE_HIP(ctx, hipMemcpyAsync(mm, d.d_minmax, sizeof(mm), hipMemcpyDeviceToHost, d.stream));
+        DCTE_HIP(ctx, hipStreamSynchronize(d.stream));
+        gmin = k == 0 ? mm[0] : (mm[0] < gmin ? mm[0] : gmin);
+        gmax = k == 0 ? mm[1] : (mm[1] > gmax ? mm[1] : gmax);
     }
     for (int k = 0; k < G; k++) {
         Device& d = ctx->devs[k];
+        int y0 = (int)((long long)h * k / G), y1 = (int)((long long)h * (k + 1) / G);
+        size_t npx = (size_t)w * (size_t)(y1 - y0);
         DCTE_HIP(ctx, hipSetDevice(d.id));
-        DCTE_HIP(ctx, hipStreamSynchronize(d.stream));
-        auto it = d.fix.find(d.stream);
-        if (it != d.fix.end()) {
-            unsigned cnt = 0;
-            DCTE_HIP(ctx, hipMemcpy(&cnt, it->second.d_count, sizeof(unsigned), hipMemcpyDeviceToHost));
-            ctx->last_refined += cnt;
-        }
+        float mm[2] = {gmin, gmax};
+        DCTE_HIP(ctx, hipMemcpyAsync(d.d_minmax, mm, sizeof(mm), hipMemcpyHostToDevice, d.stream));
+        rc = ensure_buf(ctx, (void**)&d.d_u8, &d.u8_cap, npx * channels);
+        if (rc) return rc;
+        DCTE_HIP(ctx, dcte::launch_to_u8(d.d_out, (long long)npx, d.d_minmax, mode, channels, d.d_u8, d.stream));
+        DCTE_HIP(ctx, hipMemcpyAsync(out + (size_t)y0 * w * channels, d.d_u8, npx * channels,
+                                     hipMemcpyDeviceToHost, d.stream));
     }
+    return sync_bands(ctx, G);
+}
+
+int dcte_normalize_u8(dcte_ctx* ctx, const float* E, size_t n, int mode, int channels, uint8_t* out)
+{
+    if (!ctx || !E || !out || n == 0 || !valid_norm(mode, channels)) return DCTE_EINVAL;
+    Device& d = ctx->devs[0];
+    int rc = ensure_stream(ctx, d);
+    if (rc) return rc;
+    rc = ensure_buf(ctx, (void**)&d.d_out, &d.out_cap, n * sizeof(float));
+    if (rc) return rc;
+    rc = ensure_buf(ctx, (void**)&d.d_u8, &d.u8_cap, n * channels);
+    if (rc) return rc;
+    DCTE_HIP(ctx, hipMemcpyAsync(d.d_out, E, n * sizeof(float), hipMemcpyHostToDevice, d.stream));
+    DCTE_HIP(ctx, dcte::launch_minmax(d.d_out, (long long)n, d.d_keys, d.d_minmax, d.stream));
+    DCTE_HIP(ctx, dcte::launch_to_u8(d.d_out, (long long)n, d.d_minmax, mode, channels, d.d_u8, d.stream));
+    DCTE_HIP(ctx, hipMemcpyAsync(out, d.d_u8, n * channels, hipMemcpyDeviceToHost, d.stream));
+    DCTE_HIP(ctx, hipStreamSynchronize(d.stream));
+    return DCTE_OK;
+}
+
+int dcte_minmax_device(dcte_ctx* ctx, int device, const float* d_E, long long n, float* d_minmax,
+                       void* stream)
+{
+    if (!ctx || device < 0 || device >= (int)ctx->devs.size() || !d_E || !d_minmax || n <= 0)
+        return DCTE_EINVAL;
+    Device& d = ctx->devs[device];
+    int rc = ensure_stream(ctx, d);
+    if (rc) return rc;
+    // per-stream key scratch would be needed for concurrent calls on several
+    // streams of one device; min/max calls are stream-ordered per device
+    DCTE_HIP(ctx, dcte::launch_minmax(d_E, n, d.d_keys, d_minmax, (hipStream_t)stream));
+    return DCTE_OK;
+}
+
+int dcte_normalize_u8_device(dcte_ctx* ctx, int device, const float* d_E, long long n,
+                             const float* d_minmax, int mode, int channels, uint8_t* d_out,
+                             void* stream)
+{
+    if (!ctx || device < 0 || device >= (int)ctx->devs.size() || !d_E || !d_minmax || !d_out ||
+        n <= 0 || !valid_norm(mode, channels))
+        return DCTE_EINVAL;
+    DCTE_HIP(ctx, hipSetDevice(ctx->devs[device].id));
+    DCTE_HIP(ctx, dcte::launch_to_u8(d_E, n, d_minmax, mode, channels, d_out, (hipStream_t)stream));
     return DCTE_OK;
 }
 

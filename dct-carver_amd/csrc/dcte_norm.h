@@ -1,0 +1,18 @@
+// dcte_norm.h -- launchers of the energy-map -> u8 kernels (dcte_norm.hip).
+#pragma once
+
+#include <stdint.h>
+
+#include <hip/hip_runtime.h>
+
+namespace dcte {
+
+constexpr int kNormLqr = 0;      // DCTE_NORM_LQR
+constexpr int kNormPreview = 1;  // DCTE_NORM_PREVIEW
+
+// keys: 2 device uints of scratch; minmax: 2 device floats {min, max}
+hipError_t launch_minmax(const float* e, long long n, unsigned* keys, float* minmax, hipStream_t s);
+hipError_t launch_to_u8(const float* e, long long n, const float* minmax, int mode, int channels,
+                        uint8_t* out, hipStream_t s);
+
+}  // namespace dcte

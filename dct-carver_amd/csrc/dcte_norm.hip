@@ -1,0 +1,130 @@
+// dcte_norm.hip -- energy map -> 8-bit image.
+//
+// Two passes over an HBM-resident f32 map: (1) min/max, (2) normalise to u8,
+// replicated over `channels` (the plug-in's output layer format).  Between
+// them a multi-GPU caller all-reduces the two floats (RCCL), so every band is
+// normalised with the frame's global range.
+//
+// Modes:
+//  DCTE_NORM_PREVIEW  normalize_image, src/render.c:81-109, with
+//                     DOUBLE2GUCHAR (src/render.h:6) and GIMP's ROUND:
+//                     (uint8)(int)(255 * ((d - min) / (max - min)) + 0.5) in
+//                     double; max == min (a division by zero in the
+//                     reference, src/render.c:101) gives 0.
+//  DCTE_NORM_LQR      the energy layer of display_carver_energy
+//                     (src/render.c:175-202) via lqr_carver_get_energy_image:
+//                     (E - min) / (max - min) in float, times 255, truncated
+//                     [liblqr, unverified]; max == min gives 0.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dcte_norm.h"
+
+namespace dcte {
+
+// order-preserving float <-> uint key (total order on non-NaN floats)
+__device__ __forceinline__ unsigned fkey(float f)
+{
+    unsigned b = __float_as_uint(f);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float funkey(unsigned k)
+{
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+// keys[0] = min key, keys[1] = max key; caller initialises to (~0u, 0u)
+__global__ __launch_bounds__(256) void dcte_minmax(const float* __restrict__ e, long long n,
+                                                   unsigned* keys)
+{
+    unsigned kmin = 0xffffffffu, kmax = 0u;
+    const long long stride = (long long)gridDim.x * blockDim.x * 4;
+    for (long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += stride) {
+        if (i + 3 < n) {
+            float4 v = *reinterpret_cast<const float4*>(e + i);
+            unsigned a = fkey(v.x), b = fkey(v.y), c = fkey(v.z), d = fkey(v.w);
+            kmin = min(kmin, min(min(a, b), min(c, d)));
+            kmax = max(kmax, max(max(a, b), max(c, d)));
+        } else {
+            for (long long j = i; j < n; j++) {
+                unsigned a = fkey(e[j]);
+                kmin = min(kmin, a);
+                kmax = max(kmax, a);
+            }
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        kmin = min(kmin, (unsigned)__shfl_xor((int)kmin, o));
+        kmax = max(kmax, (unsigned)__shfl_xor((int)kmax, o));
+    }
+    __shared__ unsigned smin[4], smax[4];
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        smin[wv] = kmin;
+        smax[wv] = kmax;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < 4; i++) {
+            kmin = min(kmin, smin[i]);
+            kmax = max(kmax, smax[i]);
+        }
+        atomicMin(&keys[0], kmin);
+        atomicMax(&keys[1], kmax);
+    }
+}
+
+__global__ void dcte_keys_to_floats(const unsigned* keys, float* minmax)
+{
+    minmax[0] = funkey(keys[0]);
+    minmax[1] = funkey(keys[1]);
+}
+
+__device__ __forceinline__ uint8_t norm_one(float d, float mn, float mx, int mode)
+{
+    if (!(mx > mn)) return 0;
+    if (mode == kNormPreview) {
+        double v = 255.0 * (((double)d - (double)mn) / ((double)mx - (double)mn));
+        return (uint8_t)(int)(v + 0.5);
+    }
+    float v = (d - mn) / (mx - mn);
+    return (uint8_t)(int)(v * 255.0f);
+}
+
+__global__ __launch_bounds__(256) void dcte_to_u8(const float* __restrict__ e, long long n,
+                                                  const float* minmax, int mode, int channels,
+                                                  uint8_t* __restrict__ out)
+{
+    const float mn = minmax[0], mx = minmax[1];
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint8_t v = norm_one(e[i], mn, mx, mode);
+        for (int c = 0; c < channels; c++) out[i * channels + c] = v;
+    }
+}
+
+static int grid_for(long long n)
+{
+    long long g = (n + 1023) / 1024;
+    return (int)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
+}
+
+hipError_t launch_minmax(const float* e, long long n, unsigned* keys, float* minmax, hipStream_t s)
+{
+    hipError_t err = hipMemsetAsync(keys, 0xff, sizeof(unsigned), s);
+    if (err == hipSuccess) err = hipMemsetAsync(keys + 1, 0, sizeof(unsigned), s);
+    if (err != hipSuccess) return err;
+    hipLaunchKernelGGL(dcte_minmax, dim3(grid_for(n)), dim3(256), 0, s, e, n, keys);
+    hipLaunchKernelGGL(dcte_keys_to_floats, dim3(1), dim3(1), 0, s, keys, minmax);
+    return hipGetLastError();
+}
+
+hipError_t launch_to_u8(const float* e, long long n, const float* minmax, int mode, int channels,
+                        uint8_t* out, hipStream_t s)
+{
+    hipLaunchKernelGGL(dcte_to_u8, dim3(grid_for(n)), dim3(256), 0, s, e, n, minmax, mode,
+                       channels, out);
+    return hipGetLastError();
+}
+
+}  // namespace dcte

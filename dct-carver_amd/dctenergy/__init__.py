@@ -31,12 +31,15 @@ DCTE_LQR = 0
 DCTE_PREVIEW = 1
 DCTE_OPT_TIE_TAU = 1
 DCTE_OPT_PROFILE = 2
+DCTE_NORM_LQR = 0
+DCTE_NORM_PREVIEW = 1
 
 # every symbol include/dctenergy.h declares
 EXPORTS = ("dcte_abi_version", "dcte_device_count", "dcte_create", "dcte_destroy",
            "dcte_ctx_devices", "dcte_set_option", "dcte_energy_map",
            "dcte_energy_map_device", "dcte_last_refined", "dcte_profile_read", "dcte_strerror",
-           "dcte_last_error")
+           "dcte_last_error", "dcte_normalize_u8", "dcte_energy_image_u8", "dcte_minmax_device",
+           "dcte_normalize_u8_device")
 
 _lib = None
 
@@ -90,6 +93,17 @@ def lib():
     L.dcte_profile_read.restype = ctypes.c_int
     L.dcte_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_longlong),
                                     ctypes.POINTER(ctypes.c_double)]
+    L.dcte_normalize_u8.restype = ctypes.c_int
+    L.dcte_normalize_u8.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, vp]
+    L.dcte_energy_image_u8.restype = ctypes.c_int
+    L.dcte_energy_image_u8.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_size_t, ctypes.c_int, ctypes.c_float,
+                                       ctypes.c_float, ctypes.c_int, ctypes.c_int, vp]
+    L.dcte_minmax_device.restype = ctypes.c_int
+    L.dcte_minmax_device.argtypes = [vp, ctypes.c_int, vp, ctypes.c_longlong, vp, vp]
+    L.dcte_normalize_u8_device.restype = ctypes.c_int
+    L.dcte_normalize_u8_device.argtypes = [vp, ctypes.c_int, vp, ctypes.c_longlong, vp,
+                                           ctypes.c_int, ctypes.c_int, vp, vp]
     L.dcte_strerror.restype = ctypes.c_char_p
     L.dcte_strerror.argtypes = [ctypes.c_int]
     L.dcte_last_error.restype = ctypes.c_char_p
@@ -182,6 +196,34 @@ class Context:
                                           out.ctypes.data))
         return out
 
+    # -- energy image as 8-bit grey
+    def normalize_u8(self, E, mode=DCTE_NORM_PREVIEW, channels=1):
+        E = np.ascontiguousarray(E, dtype=np.float32)
+        out = np.empty(E.shape + ((channels,) if channels > 1 else ()), np.uint8)
+        self._check(lib().dcte_normalize_u8(self._h, E.ctypes.data, E.size, mode, channels,
+                                            out.ctypes.data))
+        return out
+
+    def energy_image_u8(self, px, n=8, edges=0.5, textures=0.5, mode=DCTE_NORM_LQR, channels=1):
+        px = np.ascontiguousarray(px, dtype=np.uint8)
+        h, w = px.shape[:2]
+        bpp = 1 if px.ndim == 2 else px.shape[2]
+        out = np.empty((h, w) + ((channels,) if channels > 1 else ()), np.uint8)
+        self._check(lib().dcte_energy_image_u8(self._h, px.ctypes.data, w, h, bpp, px.strides[0],
+                                               n, edges, textures, mode, channels,
+                                               out.ctypes.data))
+        return out
+
+    def minmax_device(self, d_E, n, d_minmax, stream=0, device=0):
+        self._check(lib().dcte_minmax_device(self._h, device, ctypes.c_void_p(d_E), n,
+                                             ctypes.c_void_p(d_minmax), ctypes.c_void_p(stream)))
+
+    def normalize_u8_device(self, d_E, n, d_minmax, d_out, mode=DCTE_NORM_PREVIEW, channels=1,
+                            stream=0, device=0):
+        self._check(lib().dcte_normalize_u8_device(self._h, device, ctypes.c_void_p(d_E), n,
+                                                   ctypes.c_void_p(d_minmax), mode, channels,
+                                                   ctypes.c_void_p(d_out), ctypes.c_void_p(stream)))
+
     # -- device entry point (HBM-resident frames; addresses as ints)
     def energy_map_device(self, d_px, rowstride, w, h, bpp, in_row0, in_rows, y0, y1, n,
                           edges, textures, d_out, out_stride, stream=0, device=0):
@@ -216,4 +258,5 @@ class Context:
 
 
 __all__ = ["Context", "DcteError", "lib", "device_count", "LIB_PATH", "EXPORTS",
-           "DCTE_LQR", "DCTE_PREVIEW", "DCTE_OPT_TIE_TAU", "DCTE_OPT_PROFILE"]
+           "DCTE_LQR", "DCTE_PREVIEW", "DCTE_OPT_TIE_TAU", "DCTE_OPT_PROFILE",
+           "DCTE_NORM_LQR", "DCTE_NORM_PREVIEW"]

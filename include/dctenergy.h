@@ -111,6 +111,35 @@ int dcte_energy_map_device(dcte_ctx *ctx, int device, const void *d_px,
                            float edges, float textures, float *d_out,
                            long long out_stride, void *stream);
 
+/* ---- energy image as 8-bit grey ----------------------
+ * DCTE_NORM_PREVIEW: normalize_image (src/render.c:81-109, DOUBLE2GUCHAR of
+ *   src/render.h:6): ROUND(255*(E-min)/(max-min)) in double, replicated to
+ *   `channels` bytes per pixel; max == min -> 0 (the reference divides by
+ *   zero there, src/render.c:101).
+ * DCTE_NORM_LQR: the energy layer of display_carver_energy
+ *   (src/render.c:175-202, lqr_carver_get_energy_image): (E-min)/(max-min)
+ *   in float times 255, truncated [liblqr, unverified]. */
+#define DCTE_NORM_LQR 0
+#define DCTE_NORM_PREVIEW 1
+
+/* host buffers: E (n floats) -> out (n*channels bytes), on the first device */
+int dcte_normalize_u8(dcte_ctx *ctx, const float *E, size_t n, int mode, int channels,
+                      uint8_t *out);
+
+/* energy map + normalisation without the f32 round trip to the host: out is
+ * w*h*channels bytes.  Several devices: band maps, one global min/max. */
+int dcte_energy_image_u8(dcte_ctx *ctx, const uint8_t *px, int w, int h, int bpp,
+                         size_t rowstride, int n, float edges, float textures,
+                         int mode, int channels, uint8_t *out);
+
+/* device pieces (stream-ordered, no sync): min/max of n floats into
+ * d_minmax[0..1]; then normalise with a (possibly all-reduced) d_minmax */
+int dcte_minmax_device(dcte_ctx *ctx, int device, const float *d_E, long long n,
+                       float *d_minmax, void *stream);
+int dcte_normalize_u8_device(dcte_ctx *ctx, int device, const float *d_E, long long n,
+                             const float *d_minmax, int mode, int channels, uint8_t *d_out,
+                             void *stream);
+
 /* Pixels recomputed by the fp64 refinement in the last dcte_energy_map call
  * (diagnostic; device calls are not synchronised, so not counted). */
 long long dcte_last_refined(const dcte_ctx *ctx);

@@ -152,3 +152,28 @@ def ref_dct(win):
     d = np.array(win, dtype=np.float64, order="C")
     ref().ref_dct(d.shape[0], _ptr(d, _f64p))
     return d
+
+
+# ------------------------------------------------------- u8 normalisation
+def normalize_preview(E, channels=1):
+    """normalize_image (src/render.c:81-109) + DOUBLE2GUCHAR (src/render.h:6) +
+    GIMP ROUND ((int)(x + 0.5)), in double; max == min -> 0 (guarded)."""
+    d = np.asarray(E, dtype=np.float32).astype(np.float64)
+    mn, mx = d.min(), d.max()
+    if not mx > mn:
+        v = np.zeros(d.shape, np.uint8)
+    else:
+        v = (255 * ((d - mn) / (mx - mn)) + 0.5).astype(np.int32).astype(np.uint8)
+    return np.repeat(v[..., None], channels, -1) if channels > 1 else v
+
+
+def normalize_lqr(E, channels=1):
+    """lqr_carver_get_energy_image as documented in include/dctenergy.h
+    [liblqr, unverified]: (E - min)/(max - min) in float, x255, truncated."""
+    e = np.asarray(E, dtype=np.float32)
+    mn, mx = e.min(), e.max()
+    if not mx > mn:
+        v = np.zeros(e.shape, np.uint8)
+    else:
+        v = (((e - mn) / (mx - mn)).astype(np.float32) * np.float32(255)).astype(np.int32).astype(np.uint8)
+    return np.repeat(v[..., None], channels, -1) if channels > 1 else v

@@ -213,3 +213,25 @@ def test_ties_are_refined_to_reference(ctx):
             assert ctx.last_refined == int(EM.refine_mask(me, mt, 0.3, 0.7).sum())
             if n < 16:
                 assert ctx.last_refined > 0
+
+
+@pytest.mark.parametrize("channels", [1, 3])
+def test_normalize_u8(ctx, channels):
+    """energy map -> 8-bit image, both modes, vs numpy restatements."""
+    for entry in manifest()["maps"][:12]:
+        E = load_map(entry["output"])
+        got = ctx.normalize_u8(E, dctenergy.DCTE_NORM_PREVIEW, channels)
+        assert np.array_equal(got, O.normalize_preview(E, channels)), entry["output"]
+        got = ctx.normalize_u8(E, dctenergy.DCTE_NORM_LQR, channels)
+        assert np.array_equal(got, O.normalize_lqr(E, channels)), entry["output"]
+    flat = np.full((7, 9), 0.25, np.float32)
+    assert not ctx.normalize_u8(flat, dctenergy.DCTE_NORM_PREVIEW).any()
+
+
+def test_energy_image_u8_fused(ctx):
+    img = load_input("natural_rgb_97x41.npy")
+    E = ctx.energy_map(img, 8, 0.3, 0.7)
+    u8 = ctx.energy_image_u8(img, 8, 0.3, 0.7, dctenergy.DCTE_NORM_LQR, 1)
+    assert np.array_equal(u8, O.normalize_lqr(E))
+    u8p = ctx.energy_image_u8(img, 8, 0.3, 0.7, dctenergy.DCTE_NORM_PREVIEW, 3)
+    assert np.array_equal(u8p, O.normalize_preview(E, 3))

@@ -10,8 +10,9 @@ build() {  # name extra-flags...
   local name=$1; shift
   $HIPCC $BASE "$@" -c -o build/variants/$name.k.o csrc/dcte_kernels.hip
   $HIPCC $BASE "$@" -c -o build/variants/$name.c.o csrc/dcte_capi.cpp
-  $HIPCC --offload-arch=gfx950 -shared -o build/variants/$name.so build/variants/$name.k.o build/variants/$name.c.o
-  rm -f build/variants/$name.k.o build/variants/$name.c.o
+  $HIPCC $BASE "$@" -c -o build/variants/$name.n.o csrc/dcte_norm.hip
+  $HIPCC --offload-arch=gfx950 -shared -o build/variants/$name.so build/variants/$name.k.o build/variants/$name.n.o build/variants/$name.c.o
+  rm -f build/variants/$name.k.o build/variants/$name.c.o build/variants/$name.n.o
   echo built $name
 }
 while read -r name flags; do
