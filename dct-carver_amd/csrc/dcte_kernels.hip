@@ -61,7 +61,7 @@ struct Geo {
     static constexpr int HL = N / 2 - 1;                 // halo left / top
     static constexpr int HR = N / 2;                     // halo right / bottom
     static constexpr int LW = TW + N - 1;                // luma columns per row
-    static constexpr int LWP = LW + 1;
+    static constexpr int LWP = LW | 1;                   // odd row pitch
     static constexpr int G = (N < 8) ? 8 : (N == 8 ? DCTE_G8 : N);  // rows per group (multiple of N)
     template <int BPP>
     static constexpr int ndw() { return (LW * BPP + 3) / 4 + 1; }  // dwords per raw row
@@ -92,10 +92,14 @@ __global__ __launch_bounds__(kThreads, DCTE_MIN_WAVES) void dcte_map(const MapPa
 
     __shared__ uint32_t raw[G][NDW];
     __shared__ float lum[G][LWP];
+    // S = 4 (N = 16): per-wave partial maxima of the group's rows; only the
+    // waves owning k1 = 0 (q = 0) and k1 = 1 (q = 2) carry an edge candidate
+    __shared__ float part_t[S == 4 ? G : 1][S == 4 ? 4 : 1][S == 4 ? 64 : 1];
+    __shared__ float part_e[S == 4 ? G : 1][S == 4 ? 2 : 1][S == 4 ? 64 : 1];
 
     const int tx = threadIdx.x;
-    const int lane_p = (S == 2) ? (tx & 1) : 0;
-    const int c = (S == 2) ? (tx >> 1) : tx;         // output column within the strip
+    const int lane_p = (S == 4) ? (tx >> 6) : 0;     // N = 16: wave index = k1 class
+    const int c = (S == 4) ? (tx & 63) : tx;         // output column within the strip
     const int x0 = blockIdx.x * TW;
     const int x = x0 + c;
     const int ys = p.y0 + blockIdx.y * p.tile_h;
@@ -144,7 +148,21 @@ __global__ __launch_bounds__(kThreads, DCTE_MIN_WAVES) void dcte_map(const MapPa
     };
 
     float ring[N][CH];
-    float we = p.we, wt = p.wt;
+    const float we = p.we, wt = p.wt;
+
+    // decision + store (+ refinement flag) of output pixel (x, y)
+    auto emit = [&](int y, int xx, float mt, float me) {
+        if (xx >= w) return;
+        const bool edge = me > mt;
+        p.out[(long long)(y - p.y0) * p.out_stride + xx] = edge ? me * we : mt * wt;
+        // refine in fp64 when the class is uncertain (or, for testing,
+        // tie_tau >= 1: every pixel)
+        const float hi = fmaxf(me, mt);
+        if ((we != wt && hi > 0.0f && fabsf(me - mt) <= p.tie_tau * hi) || p.tie_tau >= 1.0f) {
+            unsigned k = atomicAdd(p.fix_count, 1u);
+            if (k < p.fix_cap) p.fix_list[k] = (unsigned)((y - p.y0) * w + xx);
+        }
+    };
 
     issue(0);
     for (int g = 0; g < ngroups; g++) {
@@ -195,26 +213,29 @@ __global__ __launch_bounds__(kThreads, DCTE_MIN_WAVES) void dcte_map(const MapPa
                 if (i >= N - 1) {
                     float mt, me;
                     Cols<N>::template run<(u + 1) % N>(ring, lane_p, mt, me);
-                    if constexpr (S == 2) {
-                        mt = fmaxf(mt, __shfl_xor(mt, 1));
-                        me = fmaxf(me, __shfl_xor(me, 1));
-                    }
-                    const int y = ys + i - (N - 1);
-                    if (x < w && lane_p == 0) {
-                        const bool edge = me > mt;
-                        p.out[(long long)(y - p.y0) * p.out_stride + x] = edge ? me * we : mt * wt;
-                        // refine in fp64 when the class is uncertain (or, for
-                        // testing, tie_tau >= 1: every pixel)
-                        const float hi = fmaxf(me, mt);
-                        if ((we != wt && hi > 0.0f && fabsf(me - mt) <= p.tie_tau * hi) ||
-                            p.tie_tau >= 1.0f) {
-                            unsigned k = atomicAdd(p.fix_count, 1u);
-                            if (k < p.fix_cap) p.fix_list[k] = (unsigned)((y - p.y0) * w + x);
-                        }
+                    if constexpr (S == 4) {
+                        part_t[u][lane_p][c] = mt;
+                        if ((lane_p & 1) == 0) part_e[u][lane_p >> 1][c] = me;
+                    } else {
+                        emit(ys + i - (N - 1), x, mt, me);
                     }
                 }
             }
         });
+        if constexpr (S == 4) {
+            // combine the four waves' maxima; wave q finishes rows u = q mod 4
+            __syncthreads();
+#pragma unroll
+            for (int u = lane_p; u < G; u += 4) {
+                const int i = g * G + u;
+                if (i >= N - 1 && i < n_in) {
+                    emit(ys + i - (N - 1), x,
+                         fmaxf(fmaxf(part_t[u][0][c], part_t[u][1][c]),
+                               fmaxf(part_t[u][2][c], part_t[u][3][c])),
+                         fmaxf(part_e[u][0][c], part_e[u][1][c]));
+                }
+            }
+        }
     }
 }
 

@@ -191,6 +191,55 @@ DCTE_HD void dct16_odd(const float d[8], float X[16])
 #undef DCTE_ROW
 }
 
+// Four odd outputs X[k0], X[k0+4], X[k0+8], X[k0+12] (k0 = 1 or 3) of the
+// 16-point transform from d_j = x_j - x_{15-j}: the rows of dct16_odd.
+DCTE_HD void dct16_odd_rows(const float d[8], int k0, float out[4])
+{
+    float X[16];
+    const float A0 = k16a0, A1 = k16a1, A2 = k16a2, A3 = k16a3;
+    const float A4 = k16a4, A5 = k16a5, A6 = k16a6, A7 = k16a7;
+#define DCTE_ROW(o, c0, c1, c2, c3, c4, c5, c6, c7)                                   \
+    X[o] = fmaf(d[7], c7, fmaf(d[6], c6, fmaf(d[5], c5, fmaf(d[4], c4,                \
+           fmaf(d[3], c3, fmaf(d[2], c2, fmaf(d[1], c1, d[0] * c0)))))));
+    if (k0 == 1) {
+        DCTE_ROW(1,  A0,  A1,  A2,  A3,  A4,  A5,  A6,  A7)
+        DCTE_ROW(5,  A2,  A7, -A3, -A1, -A6,  A4,  A0,  A5)
+        DCTE_ROW(9,  A4, -A2, -A6,  A0, -A7, -A1,  A5,  A3)
+        DCTE_ROW(13, A6, -A3,  A0, -A2,  A5,  A7, -A4,  A1)
+        out[0] = X[1]; out[1] = X[5]; out[2] = X[9]; out[3] = X[13];
+    } else {
+        DCTE_ROW(3,  A1,  A4,  A7, -A5, -A2, -A0, -A3, -A6)
+        DCTE_ROW(7,  A3, -A5, -A1,  A7,  A0,  A6, -A2, -A4)
+        DCTE_ROW(11, A5, -A0,  A4,  A6, -A1,  A3,  A7, -A2)
+        DCTE_ROW(15, A7, -A6,  A5, -A4,  A3, -A2,  A1, -A0)
+        out[0] = X[3]; out[1] = X[7]; out[2] = X[11]; out[3] = X[15];
+    }
+#undef DCTE_ROW
+}
+
+// Odd half of the 16-point transform (a DCT-IV of size 8) in 50 ops instead
+// of the 64 of dct16_odd: with a_j = pi (2j+1)/32,
+//   2 cos(a_j) cos(2k a_j) = cos((2k+1) a_j) + cos((2k-1) a_j),
+// so the 8-point DCT-II of d'_j = 2 cos(a_j) d_j gives Z_k = Y_k + Y_{k-1}
+// (Y_{-1} = Y_0), i.e. Y_0 = Z_0 / 2 and Y_m = Z_m - Y_{m-1}.  In hat units:
+//   X[1] = (g/2) E[0],  X[2m+1] = E[m] - X[2m-1]   (E = dct8(d')).
+constexpr float k16p0 = 1.9903694533443939f, k16p1 = 1.9138806714644176f;
+constexpr float k16p2 = 1.76384252869671f, k16p3 = 1.546020906725474f;
+constexpr float k16p4 = 1.268786568327291f, k16p5 = 0.9427934736519956f;
+constexpr float k16p6 = 0.5805693545089247f, k16p7 = 0.19603428065912154f;
+constexpr float k16h = 0.7071067811865476f;   // g / 2
+
+DCTE_HD void dct16_odd_fast(const float d[8], float X[16])
+{
+    float dp[8] = {d[0] * k16p0, d[1] * k16p1, d[2] * k16p2, d[3] * k16p3,
+                   d[4] * k16p4, d[5] * k16p5, d[6] * k16p6, d[7] * k16p7};
+    float E[8];
+    dct8(dp, E);
+    X[1] = E[0] * k16h;
+#pragma unroll
+    for (int m = 1; m < 8; m++) X[2 * m + 1] = E[m] - X[2 * m - 1];
+}
+
 // full 16-point transform: even half = 8-point transform of s_j = x_j + x_{15-j}
 // (same g), odd half from d_j = x_j - x_{15-j}.
 DCTE_HD void dct16(const float x[16], float X[16])
@@ -204,7 +253,23 @@ DCTE_HD void dct16(const float x[16], float X[16])
     dct8(s, E);
 #pragma unroll
     for (int m = 0; m < 8; m++) X[2 * m] = E[m];
-    dct16_odd(d, X);
+    dct16_odd_fast(d, X);
+}
+
+// max over the 16 outputs of an all-texture column, folded into m
+DCTE_HD float dct16_tex_max(const float x[16], float m)
+{
+    float s[8], d[8], X[16];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        s[j] = x[j] + x[15 - j];
+        d[j] = x[j] - x[15 - j];
+    }
+    m = dct8_tex_max(s, m);
+    dct16_odd_fast(d, X);
+#pragma unroll
+    for (int q = 1; q < 16; q += 4) m = fmaxf(fmaxf(m, fabsf(X[q])), fabsf(X[q + 2]));
+    return m;
 }
 
 }  // namespace dcte

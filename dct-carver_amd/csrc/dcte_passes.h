@@ -23,9 +23,18 @@ namespace dcte {
 
 template <int N>
 struct Lanes {
-    static constexpr int S = (N == 16) ? 2 : 1;   // lanes per output column
+    static constexpr int S = (N == 16) ? 4 : 1;   // lanes (N=16: waves) per output column
     static constexpr int CH = N / S;              // k1 channels per lane
 };
+
+// N = 16: wave q of the workgroup owns the four horizontal frequencies
+//   q = 0: k1 = 0, 4, 8, 12    (even part of the 8-point transform of s)
+//   q = 1: k1 = 2, 6, 10, 14   (odd part of the 8-point transform of s)
+//   q = 2: k1 = 1, 5, 9, 13    (odd half of the 16-point transform)
+//   q = 3: k1 = 3, 7, 11, 15
+// with s_j = x_j + x_{15-j}; channel c of wave q holds k1 = 4c + {0,2,1,3}[q].
+// Roles are wave-uniform, so nothing diverges; the four partial maxima of a
+// pixel meet in LDS (dcte_map, N = 16).
 
 // ------------------------------------------------------------------ column pass
 // Per-lane column stage: fold this lane's channels into (m_t, m_e).
@@ -85,36 +94,39 @@ template <> struct Cols<2> : ColsSmall<2> {};
 
 template <>
 struct Cols<16> {
-    // lane parity p: channel m holds k1 = 2m + p
     template <int O>
-    DCTE_HD_MEMBER void run(const float (&ring)[16][8], int p, float& mt, float& me)
+    DCTE_HD_MEMBER void run(const float (&ring)[16][4], int q, float& mt, float& me)
     {
+        float col[16], X[16];
         mt = 0.0f;
         me = 0.0f;
+        // channel 0: k1 = 4q' ... special roles for k1 = 0 (q = 0) and k1 = 1 (q = 2)
 #pragma unroll
-        for (int m = 0; m < 8; m++) {
-            float col[16], X[16];
+        for (int j = 0; j < 16; j++) col[j] = ring[(O + j) & 15][0];
+        if (q == 0) {
+            // exact integer row sums: centre on one of its own samples (exact)
+            // so no large partial sum forms; X0 is the DC (excluded), X1 = C01
+            const float ref = col[7];
 #pragma unroll
-            for (int j = 0; j < 16; j++) col[j] = ring[(O + j) & 15][m];
-            if (m == 0) {
-                // k1 = 0 column (p = 0) carries exact row sums: centre it on one
-                // of its own samples (exact) so no large partial sum forms.  The
-                // k1 = 1 column (p = 1) must keep its X0 (edge atom C10).
-                float ref = p ? 0.0f : col[7];
-#pragma unroll
-                for (int j = 0; j < 16; j++) col[j] -= ref;
-            }
+            for (int j = 0; j < 16; j++) col[j] -= ref;
             dct16(col, X);
-            if (m == 0) {
-                me = p ? fabsf(X[0]) : fabsf(X[1]);
-                float x1 = p ? fabsf(X[1]) : 0.0f;
-                mt = fmaxf(mt, x1);
+            me = fabsf(X[1]);
 #pragma unroll
-                for (int q = 2; q < 16; q++) mt = fmaxf(mt, fabsf(X[q]));
-            } else {
+            for (int k = 2; k < 16; k += 2) mt = fmaxf(fmaxf(mt, fabsf(X[k])), fabsf(X[k + 1]));
+        } else if (q == 2) {
+            dct16(col, X);                 // X0 = C10 (edge)
+            me = fabsf(X[0]);
 #pragma unroll
-                for (int q = 0; q < 16; q++) mt = fmaxf(mt, fabsf(X[q]));
-            }
+            for (int k = 1; k < 15; k += 2) mt = fmaxf(fmaxf(mt, fabsf(X[k])), fabsf(X[k + 1]));
+            mt = fmaxf(mt, fabsf(X[15]));
+        } else {
+            mt = dct16_tex_max(col, mt);
+        }
+#pragma unroll
+        for (int c = 1; c < 4; c++) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) col[j] = ring[(O + j) & 15][c];
+            mt = dct16_tex_max(col, mt);
         }
     }
 };
@@ -137,6 +149,7 @@ DCTE_HD void row_pass(const float* lrow, int c, int p, float (&dst)[Lanes<N>::CH
         float x[2] = {lrow[c], lrow[c + 1]};
         dct2(x, dst);
     } else {
+        // N = 16, wave q (see Lanes): 4 of the 16 frequencies of this row
         float s[8], d[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) {
@@ -144,13 +157,20 @@ DCTE_HD void row_pass(const float* lrow, int c, int p, float (&dst)[Lanes<N>::CH
             s[j] = a + b;
             d[j] = a - b;
         }
-        if (p == 0) {
-            dct8(s, dst);                 // k1 = 0, 2, ..., 14
+        if (p == 0 || p == 1) {
+            float t0 = s[0] + s[7], t1 = s[1] + s[6], t2 = s[2] + s[5], t3 = s[3] + s[4];
+            if (p == 0) {                   // k1 = 0, 4, 8, 12 (exact sums for 0, 8)
+                float a = t0 + t3, b = t1 + t2, cc = t0 - t3, e = t1 - t2;
+                dst[0] = a + b;
+                dst[1] = fmaf(cc, k8E, e * k8F);
+                dst[2] = a - b;
+                dst[3] = fmaf(cc, k8F, -(e * k8E));
+            } else {                        // k1 = 2, 6, 10, 14
+                dct8_odd(s[0] - s[7], s[1] - s[6], s[2] - s[5], s[3] - s[4],
+                         dst[0], dst[1], dst[2], dst[3]);
+            }
         } else {
-            float X[16];
-            dct16_odd(d, X);              // k1 = 1, 3, ..., 15
-#pragma unroll
-            for (int m = 0; m < 8; m++) dst[m] = X[2 * m + 1];
+            dct16_odd_rows(d, p == 2 ? 1 : 3, dst);   // k1 = 1,5,9,13 or 3,7,11,15
         }
     }
 }

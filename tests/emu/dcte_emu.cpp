@@ -30,7 +30,7 @@ void pixel(const uint8_t* px, int w, int h, int bpp, size_t rs, int x, int y, fl
     constexpr int CH = Lanes<N>::CH, S = Lanes<N>::S;
     float lrow[N];
     float ring[N][CH];
-    float mts[2] = {0, 0}, mes[2] = {0, 0};
+    float mts[4] = {0, 0, 0, 0}, mes[4] = {0, 0, 0, 0};
     for (int lp = 0; lp < S; lp++) {
         for (int j = 0; j < N; j++) {   // input row y - (N/2 - 1) + j -> slot j
             int t = clampi(y - (N / 2 - 1) + j, 0, h - 1);
@@ -42,8 +42,8 @@ void pixel(const uint8_t* px, int w, int h, int bpp, size_t rs, int x, int y, fl
         }
         Cols<N>::template run<0>(ring, lp, mts[lp], mes[lp]);
     }
-    mt = fmaxf(mts[0], mts[1]);
-    me = fmaxf(mes[0], mes[1]);
+    mt = fmaxf(fmaxf(mts[0], mts[1]), fmaxf(mts[2], mts[3]));
+    me = fmaxf(fmaxf(mes[0], mes[1]), fmaxf(mes[2], mes[3]));
 }
 
 }  // namespace
