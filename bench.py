@@ -42,6 +42,12 @@ def parse():
     ap.add_argument("--textures", type=float, default=0.7)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=512)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: stage halos through host memory (rehearsal of the N>1 path "
+                         "on a box with fewer GPUs than ranks)")
+    ap.add_argument("--check", action="store_true",
+                    help="after timing, recompute every band from regenerated rows (no "
+                         "exchange) and require bit-equality")
     return ap.parse_args()
 
 
@@ -94,10 +100,15 @@ def main():
             print("bench: --gpus N > 1 needs torch.distributed.run (one process per GPU)",
                   file=sys.stderr)
             sys.exit(2)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    gpu = local % max(1, ndev)          # == local on a full node
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     n, S = args.n, args.size
     H, W = world * S, S
@@ -115,7 +126,7 @@ def main():
     # a context over the visible devices (state is created lazily, only on the
     # device this rank uses); device index = this rank's local device
     ctx = dctenergy.Context(ngpus=0)
-    dev_index = local
+    dev_index = gpu
 
     stream = torch.cuda.current_stream(dev).cuda_stream
     e, t = args.edges, args.textures
@@ -129,11 +140,29 @@ def main():
                               n, e, t, out[y0 - band.Y0:].data_ptr(), out.stride(0), stream,
                               dev_index)
 
+    host_buf = None
+    if world > 1 and args.dist_backend == "gloo":
+        host_buf = torch.empty(buf.shape, dtype=torch.uint8, pin_memory=True)
+
     def step():
-        reqs = D.exchange_halos(buf, band) if world > 1 else []
-        run_rows(i0, i1)                    # overlaps the exchange
-        for r in reqs:
-            r.wait()                        # current stream waits for the halos
+        if world > 1 and host_buf is not None:
+            # rehearsal path: halo rows via host memory and gloo
+            run_rows(i0, i1)
+            t0_, o_ = band.top, band.own
+            host_buf[t0_:t0_ + band.hr].copy_(buf[t0_:t0_ + band.hr])          # to rank-1
+            if band.hl:
+                host_buf[t0_ + o_ - band.hl:t0_ + o_].copy_(buf[t0_ + o_ - band.hl:t0_ + o_])
+            for r in D.exchange_halos(host_buf, band):
+                r.wait()
+            if band.top:
+                buf[:band.top].copy_(host_buf[:band.top], non_blocking=True)
+            if band.bot:
+                buf[band.rows - band.bot:].copy_(host_buf[band.rows - band.bot:], non_blocking=True)
+        else:
+            reqs = D.exchange_halos(buf, band) if world > 1 else []
+            run_rows(i0, i1)                # overlaps the exchange
+            for r in reqs:
+                r.wait()                    # current stream waits for the halos
         for a, b in band.edges():
             run_rows(a, b)
 
@@ -155,7 +184,8 @@ def main():
     launches, kern_ms = ctx.profile_read()
     ctx.set_option(dctenergy.DCTE_OPT_PROFILE, 0)
     # interior launch is the dominant kernel; edge launches are a few rows
-    stats = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    stats = torch.tensor([elapsed], dtype=torch.float64,
+                         device="cpu" if args.dist_backend == "gloo" else dev)
     if world > 1:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
     elapsed = float(stats[0])
@@ -172,6 +202,22 @@ def main():
     pmc = _pmc(n, S)
     valu_per_px = pmc.get("valu_lane_ops_per_px")
     valu_rate = (px_per_rank * valu_per_px / (kernel_ms_per_step * 1e-3)) if valu_per_px else None
+
+    check = None
+    if args.check:
+        # regenerate this band's rows INCLUDING the halo rows straight from the
+        # global frame definition and recompute without any exchange
+        ref_in = synth.natural_rows(band.row0, band.rows, W, 3, seed=0, device=dev)
+        ref_out = torch.empty_like(out)
+        ctx.energy_map_device(ref_in.data_ptr(), ref_in.stride(0), W, H, 3, band.row0, band.rows,
+                              band.Y0, band.Y1, n, e, t, ref_out.data_ptr(), ref_out.stride(0),
+                              stream, dev_index)
+        torch.cuda.synchronize()
+        ok = torch.tensor([1 if (torch.equal(ref_out, out) and torch.equal(ref_in, buf)) else 0],
+                          dtype=torch.int64, device="cpu" if args.dist_backend == "gloo" else dev)
+        if world > 1:
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        check = bool(ok.item())
 
     if rank == 0:
         res = {
@@ -217,6 +263,10 @@ def main():
                           "peak = 256 CU x 4 SIMD x 64 lanes / 2 cyc x 2.4 GHz",
             },
         }
+        if check is not None:
+            res["check_bands_bit_exact"] = check
+        if world > 1 and args.dist_backend != "nccl":
+            res["config"]["parallelism"] += f" (halo via {args.dist_backend} rehearsal)"
         if world == 1 and not args.no_cpu_baseline:
             host = buf[:args.cpu_rows + n].cpu().numpy()
             res["cpu_baseline"] = cpu_baseline(host, W, n, e, t, args.cpu_rows)
