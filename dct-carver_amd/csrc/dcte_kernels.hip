@@ -240,26 +240,86 @@ __global__ __launch_bounds__(kThreads, DCTE_MIN_WAVES) void dcte_map(const MapPa
 }
 
 // ------------------------------------------------------------------ refinement
+// One wave per flagged pixel: the N*N window is gathered in parallel (one
+// element per lane), each 1-D pass of the reference transform runs on N lanes
+// (one lane per line, the reference's own operation sequence, fp64, in LDS),
+// and the last-maximum scan of src/dct.c:116-124 becomes an exact reduction:
+// M = max |C| over the non-DC coefficients, and the winner is the LARGEST
+// linear index k1*N + k2 with |C| == M (that is what "max <= currval" keeps).
+constexpr int kFixWaves = 4;
+
 template <int N>
-__global__ __launch_bounds__(64) void dcte_fix(const FixParams p)
+__global__ __launch_bounds__(64 * kFixWaves) void dcte_fix(const FixParams p)
 {
+    __shared__ double win[kFixWaves][N * N];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double* d = win[wv];
     const unsigned cnt = min(*p.fix_count, p.fix_cap);
     constexpr int r = N / 2;
-    for (unsigned k = blockIdx.x * blockDim.x + threadIdx.x; k < cnt; k += gridDim.x * blockDim.x) {
+    for (unsigned k = blockIdx.x * kFixWaves + wv; k < cnt; k += gridDim.x * kFixWaves) {
         const unsigned idx = p.fix_list[k];
         const int y = p.y0 + (int)(idx / (unsigned)p.w);
         const int x = (int)(idx % (unsigned)p.w);
-        double d[N * N];
-        for (int i = -r + 1; i <= r; i++) {
-            const int xx = clampi(x + i, 0, p.w - 1);
-            for (int j = -r + 1; j <= r; j++) {
-                const int yy = clampi(y + j, 0, p.h - 1);
-                const uint8_t* px = p.px + (long long)(yy - p.in_row0) * p.rowstride + (long long)xx * p.bpp;
-                d[(i + r - 1) * N + (j + r - 1)] = r64::luma(px, p.bpp);
+        for (int e = lane; e < N * N; e += 64) {
+            const int i = e / N, j = e % N;          // d[i][j], i = x offset
+            const int xx = clampi(x + i - (r - 1), 0, p.w - 1);
+            const int yy = clampi(y + j - (r - 1), 0, p.h - 1);
+            const uint8_t* px = p.px + (long long)(yy - p.in_row0) * p.rowstride + (long long)xx * p.bpp;
+            d[e] = r64::luma(px, p.bpp);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if constexpr (N == 8 || N == 16) {
+            // ddct8x8s / ddct16x16s: along the first index, then the second
+            if (lane < N) {
+                if constexpr (N == 8) r64::step8(d + lane, N); else r64::step16(d + lane, N);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane < N) {
+                if constexpr (N == 8) r64::step8(d + N * lane, 1); else r64::step16(d + N * lane, 1);
+            }
+        } else {
+            // ddct2d: rows (second index) first, then columns
+            if (lane < N) r64::step_small(N, d + N * lane, 1, p.ct);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane < N) r64::step_small(N, d + lane, N, p.ct);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // exact last-maximum reduction
+        double best = -1.0;
+        int bi = -1;
+        for (int e = lane; e < N * N; e += 64) {
+            if (e == 0) continue;                     // DC (k1 || k2)
+            double v = fabs(d[e]);
+            if (v >= best) {                          // later e wins ties
+                best = v;
+                bi = e;
             }
         }
-        r64::transform(N, d, p.ct);
-        p.out[(long long)(y - p.y0) * p.out_stride + x] = r64::weighted_max(N, d, p.edges, p.textures);
+        for (int o = 32; o > 0; o >>= 1) {
+            double ob = __shfl_xor(best, o);
+            int oi = __shfl_xor(bi, o);
+            if (ob > best || (ob == best && oi > bi)) {
+                best = ob;
+                bi = oi;
+            }
+        }
+        if (lane == 0) {
+            const int k1 = bi / N, k2 = bi % N;
+            const bool edge = (k1 == 0 && k2 == 1) || (k1 == 1 && k2 == 0);
+            p.out[(long long)(y - p.y0) * p.out_stride + x] =
+                edge ? (float)(best * (double)p.edges) : (float)(best * (double)p.textures);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 
@@ -293,7 +353,7 @@ hipError_t launch_map(int n, int bpp, const MapParams& p, hipStream_t s)
 
 hipError_t launch_fix(const FixParams& p, hipStream_t s)
 {
-    dim3 grid(256), block(64);
+    dim3 grid(256), block(64 * kFixWaves);
     switch (p.n) {
     case 2: hipLaunchKernelGGL(dcte_fix<2>, grid, block, 0, s, p); break;
     case 4: hipLaunchKernelGGL(dcte_fix<4>, grid, block, 0, s, p); break;
