@@ -135,6 +135,8 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     if (span >= (1LL << 32)) return DCTE_ERANGE;
     size_t npix = (size_t)(y1 - y0) * (size_t)w;
     if (npix >= (1ULL << 32)) return DCTE_ERANGE;
+    // one workgroup's output rows go through one buffer resource
+    if ((long long)dcte::map_default_tile_h(n) * out_stride * 4 >= (1LL << 31)) return DCTE_ERANGE;
 
     DCTE_HIP(ctx, hipSetDevice(d.id));
     FixScratch* f = nullptr;

@@ -149,20 +149,29 @@ __global__ __launch_bounds__(kThreads, DCTE_MIN_WAVES) void dcte_map(const MapPa
 
     float ring[N][CH];
     const float we = p.we, wt = p.wt;
+    // output rows [ys, ye) of this workgroup through one buffer resource
+    const int ostride4 = (int)(p.out_stride * 4);
+    __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+        p.out + (long long)(ys - p.y0) * p.out_stride, (short)0,
+        (int)((unsigned)(max(ye - ys - 1, 0)) * (unsigned)ostride4 + (unsigned)w * 4u), (int)kBufFlags);
+    const bool check_ties = we != wt;                // uniform
+    const bool force_all = p.tie_tau >= 1.0f;        // uniform
+    const float keep = 1.0f - p.tie_tau;             // |me - mt| <= tau * hi  <=>  lo >= (1 - tau) hi
 
     // decision + store (+ refinement flag) of output pixel (x, y)
     auto emit = [&](int y, int xx, float mt, float me) {
         if (xx >= w) return;
-        const bool edge = me > mt;
-        p.out[(long long)(y - p.y0) * p.out_stride + xx] = edge ? me * we : mt * wt;
-        // refine in fp64 when the class is uncertain (or, for testing,
-        // tie_tau >= 1: every pixel)
-        const float hi = fmaxf(me, mt);
-        if ((we != wt && hi > 0.0f && fabsf(me - mt) <= p.tie_tau * hi) || p.tie_tau >= 1.0f) {
+        const float hi = fmaxf(me, mt), lo = fminf(me, mt);
+        // row offset is wave-uniform (soffset), column offset per lane
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hi * (me > mt ? we : wt)), orsrc,
+                                              xx * 4, (y - ys) * ostride4, 0);
+        // refine in fp64 when the class is uncertain: lo within the fp32
+        // error band of hi (never for all-zero windows); every pixel when
+        // tie_tau >= 1 (testing)
+        if ((check_ties && lo > keep * hi) || force_all) {
             unsigned k = atomicAdd(p.fix_count, 1u);
             if (k < p.fix_cap) p.fix_list[k] = (unsigned)((y - p.y0) * w + xx);
-        }
-    };
+        }    };
 
     issue(0);
     for (int g = 0; g < ngroups; g++) {

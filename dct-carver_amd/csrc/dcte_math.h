@@ -35,6 +35,9 @@
 
 namespace dcte {
 
+// running max folding two more magnitudes in: one v_max3_f32 (abs modifiers)
+DCTE_HD float max2in(float m, float a, float b) { return fmaxf(fmaxf(m, fabsf(a)), fabsf(b)); }
+
 // ---------------------------------------------------------------- N = 8
 // g * cos(pi (2j+1) k / 16) magnitudes (g = sqrt 2)
 constexpr float k8A = 1.3870398453221475f;   // cos(1 pi/16)
@@ -54,21 +57,13 @@ DCTE_HD void dct8_odd(float d0, float d1, float d2, float d3,
     X7 = fmaf(d3, -k8A, fmaf(d2, k8B, fmaf(d1, -k8C, d0 * k8D)));
 }
 
-// max(|X1|, |X3|, |X5|, |X7|) folded into m, via two rotations:
+// Odd outputs for the max (used inline by the *_max columns below): two
+// rotations
 //   t0 = C d0 + B d3, t3 = C d3 - B d0, t1 = D d1 + A d2, t2 = D d2 - A d1
-//   X3 = -(t3 + t1), X5 = t0 + t2, X1,7 = (P +- Q)/sqrt2, P = t1 - t3, Q = t0 - t2
-// and max(|P + Q|, |P - Q|) = |P| + |Q|: 14 VALU ops for the four outputs.
+// give X3 = -(t3 + t1), X5 = t0 + t2, X1,7 = (P +- Q)/sqrt2 with P = t1 - t3,
+// Q = t0 - t2, and max(|P + Q|, |P - Q|) = |P| + |Q|: 14 VALU ops for the
+// four outputs instead of 16, and three values to fold instead of four.
 constexpr float k8R = 0.7071067811865475f;  // 1/sqrt2
-DCTE_HD float dct8_odd_max(float d0, float d1, float d2, float d3, float m)
-{
-    float t0 = fmaf(d3, k8B, d0 * k8C);
-    float t3 = fmaf(d0, -k8B, d3 * k8C);
-    float t1 = fmaf(d2, k8A, d1 * k8D);
-    float t2 = fmaf(d1, -k8A, d2 * k8D);
-    float pq = (fabsf(t1 - t3) + fabsf(t0 - t2)) * k8R;
-    float X3 = t3 + t1, X5 = t0 + t2;
-    return fmaxf(fmaxf(m, pq), fmaxf(fabsf(X3), fabsf(X5)));
-}
 
 // full 8-point transform (first pass, and k1 >= 1 columns of the second)
 DCTE_HD void dct8(const float x[8], float X[8])
@@ -97,8 +92,14 @@ DCTE_HD float dct8_tex_max(const float x[8], float m)
     float X04 = fabsf(a) + fabsf(b);
     float X2 = fmaf(c, k8E, e * k8F);
     float X6 = fmaf(c, k8F, -(e * k8E));
-    m = fmaxf(fmaxf(m, X04), fmaxf(fabsf(X2), fabsf(X6)));
-    return dct8_odd_max(d0, d1, d2, d3, m);
+    float t0 = fmaf(d3, k8B, d0 * k8C);
+    float t3 = fmaf(d0, -k8B, d3 * k8C);
+    float t1 = fmaf(d2, k8A, d1 * k8D);
+    float t2 = fmaf(d1, -k8A, d2 * k8D);
+    float pq = (fabsf(t1 - t3) + fabsf(t0 - t2)) * k8R;
+    m = max2in(m, X04, X2);
+    m = max2in(m, X6, pq);
+    return max2in(m, t3 + t1, t0 + t2);
 }
 
 // k1 = 1 column: X[0] is the edge atom (1,0); X[1..7] are textures.
@@ -110,11 +111,16 @@ DCTE_HD float dct8_k1_max(const float x[8], float m, float& edge)
     float s3 = x[3] + x[4], d3 = x[3] - x[4];
     float a = s0 + s3, b = s1 + s2, c = s0 - s3, e = s1 - s2;
     edge = fabsf(a + b);
-    float X4 = a - b;
     float X2 = fmaf(c, k8E, e * k8F);
     float X6 = fmaf(c, k8F, -(e * k8E));
-    m = fmaxf(fmaxf(m, fabsf(X4)), fmaxf(fabsf(X2), fabsf(X6)));
-    return dct8_odd_max(d0, d1, d2, d3, m);
+    float t0 = fmaf(d3, k8B, d0 * k8C);
+    float t3 = fmaf(d0, -k8B, d3 * k8C);
+    float t1 = fmaf(d2, k8A, d1 * k8D);
+    float t2 = fmaf(d1, -k8A, d2 * k8D);
+    float pq = (fabsf(t1 - t3) + fabsf(t0 - t2)) * k8R;
+    m = max2in(m, a - b, X2);
+    m = max2in(m, X6, pq);
+    return max2in(m, t3 + t1, t0 + t2);
 }
 
 // k1 = 0 column (inputs: exact integer row sums, |x| <= 5.1e6).  X[0] (the
@@ -133,9 +139,9 @@ DCTE_HD float dct8_k0_max(const float x[8], float m, float& edge)
     float X1, X3, X5, X7;
     dct8_odd(d0, d1, d2, d3, X1, X3, X5, X7);
     edge = fabsf(X1);
-    m = fmaxf(fmaxf(m, fabsf(X4)), fabsf(X2));
-    m = fmaxf(fmaxf(m, fabsf(X6)), fabsf(X3));
-    return fmaxf(fmaxf(m, fabsf(X5)), fabsf(X7));
+    m = max2in(m, X4, X2);
+    m = max2in(m, X6, X3);
+    return max2in(m, X5, X7);
 }
 
 // ---------------------------------------------------------------- N = 4, 2

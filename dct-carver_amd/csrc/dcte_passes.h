@@ -43,17 +43,15 @@ struct Cols;
 
 template <>
 struct Cols<8> {
-    // ring[s][k1]; oldest row in slot O
+    // ring[s][k1]; oldest row in slot O.  k1 = 0 first (m starts at 0)
     template <int O>
-    DCTE_HD_MEMBER void run(const float (&ring)[8][8], int /*lane_p*/,
-                                               float& mt, float& me)
+    DCTE_HD_MEMBER void run(const float (&ring)[8][8], int /*lane_p*/, float& mt, float& me)
     {
         float col[8];
         float e0, e1;
-        mt = 0.0f;
 #pragma unroll
         for (int j = 0; j < 8; j++) col[j] = ring[(O + j) & 7][0];
-        mt = dct8_k0_max(col, mt, e0);
+        mt = dct8_k0_max(col, 0.0f, e0);
 #pragma unroll
         for (int j = 0; j < 8; j++) col[j] = ring[(O + j) & 7][1];
         mt = dct8_k1_max(col, mt, e1);

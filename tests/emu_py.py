@@ -61,4 +61,5 @@ def refine_mask(me, mt, edges, textures, tau=TIE_TAU):
     if np.float32(edges) == np.float32(textures):
         return np.zeros(me.shape, bool)
     hi = np.maximum(me, mt)
-    return (hi > 0) & (np.abs(me - mt) <= np.float32(tau) * hi)
+    lo = np.minimum(me, mt)
+    return lo > (np.float32(1) - np.float32(tau)) * hi
