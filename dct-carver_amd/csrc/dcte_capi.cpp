@@ -77,12 +77,27 @@ int hip_fail(dcte_ctx* ctx, hipError_t e, const char* where)
 
 bool valid_n(int n) { return n == 2 || n == 4 || n == 8 || n == 16; }
 
-// rows the clamp can touch for output rows [y0, y1)
-void needed_rows(int n, int h, int y0, int y1, int& lo, int& hi)
+// window offsets -hl .. +hr of a semantics
+void halo(int n, int sem, int& hl, int& hr)
 {
-    int r = n / 2;
-    lo = y0 - (r - 1) < 0 ? 0 : y0 - (r - 1);
-    hi = y1 - 1 + r > h - 1 ? h - 1 : y1 - 1 + r;
+    hl = sem == DCTE_LQR ? n / 2 - 1 : (n - 1) / 2 - 1;
+    hr = n - 1 - hl;
+}
+
+// rows the clamp can touch for output rows [y0, y1)
+void needed_rows(int n, int sem, int h, int y0, int y1, int& lo, int& hi)
+{
+    int hl, hr;
+    halo(n, sem, hl, hr);
+    lo = y0 - hl < 0 ? 0 : (y0 - hl > h - 1 ? h - 1 : y0 - hl);
+    hi = y1 - 1 + hr > h - 1 ? h - 1 : (y1 - 1 + hr < 0 ? 0 : y1 - 1 + hr);
+}
+
+bool valid_sem_bpp(int sem, int bpp)
+{
+    if (sem == DCTE_LQR) return bpp == 1 || bpp == 3;
+    if (sem == DCTE_PREVIEW) return bpp == 1 || bpp == 3 || bpp == 4;
+    return false;
 }
 
 int ensure_fix(dcte_ctx* ctx, Device& d, hipStream_t s, size_t npix, FixScratch** out)
@@ -121,14 +136,14 @@ void small_twiddles(int n, double ct[4])
 
 int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, int w, int h,
                int bpp, int in_row0, int in_rows, int y0, int y1, int n, float edges,
-               float textures, float* d_out, long long out_stride, hipStream_t s)
+               float textures, int sem, float* d_out, long long out_stride, hipStream_t s)
 {
-    if (!valid_n(n) || (bpp != 1 && bpp != 3) || w <= 0 || h <= 0) return DCTE_EINVAL;
+    if (!valid_n(n) || !valid_sem_bpp(sem, bpp) || w <= 0 || h <= 0) return DCTE_EINVAL;
     if (y0 < 0 || y1 > h || y0 > y1 || !d_px || !d_out || out_stride < w) return DCTE_EINVAL;
     if (rowstride < (long long)w * bpp) return DCTE_EINVAL;
     if (y1 == y0) return DCTE_OK;
     int lo, hi;
-    needed_rows(n, h, y0, y1, lo, hi);
+    needed_rows(n, sem, h, y0, y1, lo, hi);
     if (lo < in_row0 || hi >= in_row0 + in_rows) return DCTE_EINVAL;
     // one buffer resource addresses the readable rows: < 4 GiB
     long long span = (long long)(in_rows - 1) * rowstride + (long long)w * bpp + 3;
@@ -143,7 +158,8 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     int rc = ensure_fix(ctx, d, s, npix, &f);
     if (rc) return rc;
 
-    const double scale = dcte::kLumaScale * (n >= 8 ? (double)n : 1.0);
+    // hat units (dcte_math.h): C * (N or 1); luma units: 1/1275000 (liblqr) or u8
+    const double scale = (sem == DCTE_LQR ? dcte::kLumaScale : 1.0) * (n >= 8 ? (double)n : 1.0);
     dcte::MapParams p{};
     p.px = static_cast<const uint8_t*>(d_px);
     p.rowstride = rowstride;
@@ -174,6 +190,7 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     q.bpp = bpp;
     q.n = n;
     q.y0 = y0;
+    q.sem = sem;
     q.out = d_out;
     q.out_stride = out_stride;
     q.edges = edges;
@@ -189,11 +206,11 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
         DCTE_HIP(ctx, hipEventCreate(&ev.a));
         DCTE_HIP(ctx, hipEventCreate(&ev.b));
         DCTE_HIP(ctx, hipEventRecord(ev.a, s));
-        DCTE_HIP(ctx, dcte::launch_map(n, bpp, p, s));
+        DCTE_HIP(ctx, dcte::launch_map(n, bpp, sem, p, s));
         DCTE_HIP(ctx, hipEventRecord(ev.b, s));
         ctx->prof.push_back(ev);
     } else {
-        DCTE_HIP(ctx, dcte::launch_map(n, bpp, p, s));
+        DCTE_HIP(ctx, dcte::launch_map(n, bpp, sem, p, s));
     }
     if ((p.we != p.wt && ctx->tie_tau > 0) || ctx->tie_tau >= 1.0)
         DCTE_HIP(ctx, dcte::launch_fix(q, s));
@@ -230,7 +247,7 @@ bool valid_norm(int mode, int channels)
 // host frame -> device band maps (rows split over the context's devices),
 // left on the devices in d.d_out; returns the number of devices used
 int map_bands(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride, int n,
-              float edges, float textures, int* used)
+              float edges, float textures, int sem, int* used)
 {
     const int G = (int)ctx->devs.size() < h ? (int)ctx->devs.size() : h;
     const size_t pitch = (size_t)w * bpp;
@@ -238,7 +255,7 @@ int map_bands(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t ro
         Device& d = ctx->devs[k];
         int y0 = (int)((long long)h * k / G), y1 = (int)((long long)h * (k + 1) / G);
         int lo, hi;
-        needed_rows(n, h, y0, y1, lo, hi);
+        needed_rows(n, sem, h, y0, y1, lo, hi);
         size_t in_bytes = pitch * (size_t)(hi - lo + 1);
         size_t out_bytes = sizeof(float) * (size_t)w * (size_t)(y1 - y0);
         int rc = ensure_stream(ctx, d);
@@ -250,7 +267,7 @@ int map_bands(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t ro
         DCTE_HIP(ctx, hipMemcpy2DAsync(d.d_in, pitch, px + (size_t)lo * rowstride, rowstride,
                                        pitch, hi - lo + 1, hipMemcpyHostToDevice, d.stream));
         rc = run_device(ctx, d, d.d_in, (long long)pitch, w, h, bpp, lo, hi - lo + 1, y0, y1, n,
-                        edges, textures, d.d_out, w, d.stream);
+                        edges, textures, sem, d.d_out, w, d.stream);
         if (rc) return rc;
     }
     *used = G;
@@ -344,25 +361,24 @@ int dcte_set_option(dcte_ctx* ctx, int option, double value)
 
 int dcte_energy_map_device(dcte_ctx* ctx, int device, const void* d_px, long long rowstride,
                            int w, int h, int bpp, int in_row0, int in_rows, int y0, int y1,
-                           int n, float edges, float textures, float* d_out,
+                           int n, float edges, float textures, int semantics, float* d_out,
                            long long out_stride, void* stream)
 {
     if (!ctx || device < 0 || device >= (int)ctx->devs.size()) return DCTE_EINVAL;
     return run_device(ctx, ctx->devs[device], d_px, rowstride, w, h, bpp, in_row0, in_rows, y0,
-                      y1, n, edges, textures, d_out, out_stride, (hipStream_t)stream);
+                      y1, n, edges, textures, semantics, d_out, out_stride, (hipStream_t)stream);
 }
 
 int dcte_energy_map(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride,
                     int n, float edges, float textures, int semantics, int transposed, float* out)
 {
     if (!ctx || !px || !out) return DCTE_EINVAL;
-    if (!valid_n(n) || (bpp != 1 && bpp != 3) || w <= 0 || h <= 0) return DCTE_EINVAL;
+    if (!valid_n(n) || !valid_sem_bpp(semantics, bpp) || w <= 0 || h <= 0) return DCTE_EINVAL;
     if (rowstride < (size_t)w * bpp) return DCTE_EINVAL;
-    if (semantics != DCTE_LQR) return semantics == DCTE_PREVIEW ? DCTE_ENOTSUP : DCTE_EINVAL;
     if (transposed) return DCTE_ENOTSUP;
     ctx->last_refined = 0;
     int G = 0;
-    int rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, &G);
+    int rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, &G);
     if (rc) return rc;
     for (int k = 0; k < G; k++) {
         Device& d = ctx->devs[k];
@@ -376,15 +392,15 @@ int dcte_energy_map(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, siz
 }
 
 int dcte_energy_image_u8(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp,
-                         size_t rowstride, int n, float edges, float textures, int mode,
-                         int channels, uint8_t* out)
+                         size_t rowstride, int n, float edges, float textures, int semantics,
+                         int mode, int channels, uint8_t* out)
 {
     if (!ctx || !px || !out) return DCTE_EINVAL;
-    if (!valid_n(n) || (bpp != 1 && bpp != 3) || w <= 0 || h <= 0) return DCTE_EINVAL;
+    if (!valid_n(n) || !valid_sem_bpp(semantics, bpp) || w <= 0 || h <= 0) return DCTE_EINVAL;
     if (rowstride < (size_t)w * bpp || !valid_norm(mode, channels)) return DCTE_EINVAL;
     ctx->last_refined = 0;
     int G = 0;
-    int rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, &G);
+    int rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, &G);
     if (rc) return rc;
     // per-band min/max, reduced on the host (2 floats per device)
     float gmin = 0, gmax = 0;

@@ -34,6 +34,7 @@ struct FixParams {
     const uint8_t* px;
     long long rowstride;
     int w, h, in_row0, bpp, n, y0;
+    int sem;                 // kSemLqr / kSemPreview
     float* out;
     long long out_stride;
     float edges, textures;
@@ -44,7 +45,7 @@ struct FixParams {
 };
 
 // host-side launchers (dcte_kernels.hip)
-hipError_t launch_map(int n, int bpp, const MapParams& p, hipStream_t s);
+hipError_t launch_map(int n, int bpp, int sem, const MapParams& p, hipStream_t s);
 hipError_t launch_fix(const FixParams& p, hipStream_t s);
 
 // geometry the launcher uses (exported for tests / bench)

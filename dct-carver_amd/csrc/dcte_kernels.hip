@@ -53,18 +53,25 @@ constexpr int kThreads = 256;
 #endif
 constexpr unsigned kBufFlags = 0x00020000u;  // gfx9 raw buffer dword3
 
-template <int N>
+// SEM = kSemLqr    : liblqr callback window, offsets -(N/2-1)..N/2
+//                    (src/render.c:146-152), liblqr luma (dcte_luma.h)
+// SEM = kSemPreview: GTK preview window, offsets -(c-1)..N-c with
+//                    c = (N-1)/2 (src/dct.h:8-9, src/render.c:43-44, 461),
+//                    u8 luma RGB2LUMINANCE (src/render.h:5)
+template <int N, int SEM>
 struct Geo {
     static constexpr int S = Lanes<N>::S;                // lanes per output column
     static constexpr int CH = Lanes<N>::CH;              // k1 channels per lane
     static constexpr int TW = kThreads / S;              // output columns per WG
-    static constexpr int HL = N / 2 - 1;                 // halo left / top
-    static constexpr int HR = N / 2;                     // halo right / bottom
+    static constexpr int HL = SEM == kSemLqr ? N / 2 - 1 : (N - 1) / 2 - 1;   // halo left / top
+    static constexpr int HR = N - 1 - HL;                                     // halo right / bottom
     static constexpr int LW = TW + N - 1;                // luma columns per row
     static constexpr int LWP = LW | 1;                   // odd row pitch
     static constexpr int G = (N < 8) ? 8 : (N == 8 ? DCTE_G8 : N);  // rows per group (multiple of N)
     template <int BPP>
     static constexpr int ndw() { return (LW * BPP + 3) / 4 + 1; }  // dwords per raw row
+    template <int BPP>
+    static constexpr int dpt() { return (ndw<BPP>() + kThreads - 1) / kThreads; }  // per lane
 };
 
 template <int... Is, class F>
@@ -81,14 +88,14 @@ __device__ __forceinline__ void static_for(F&& f)
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 // ------------------------------------------------------------------ main kernel
-template <int N, int BPP>
+template <int N, int BPP, int SEM>
 __global__ __launch_bounds__(kThreads, DCTE_MIN_WAVES) void dcte_map(const MapParams p)
 {
-    using Gm = Geo<N>;
+    using Gm = Geo<N, SEM>;
     constexpr int S = Gm::S, CH = Gm::CH, TW = Gm::TW, HL = Gm::HL;
     constexpr int LW = Gm::LW, LWP = Gm::LWP, G = Gm::G;
     constexpr int NDW = Gm::template ndw<BPP>();
-    static_assert(NDW <= kThreads, "one raw dword per lane per row");
+    constexpr int DPT = Gm::template dpt<BPP>();         // raw dwords per lane per row
 
     __shared__ uint32_t raw[G][NDW];
     __shared__ float lum[G][LWP];
@@ -109,7 +116,7 @@ __global__ __launch_bounds__(kThreads, DCTE_MIN_WAVES) void dcte_map(const MapPa
     const int w = p.w, h = p.h;
 
     // raw byte span of one input row: columns [xs, xs + span) of the strip
-    const int xs = max(0, x0 - HL);
+    const int xs = min(max(0, x0 - HL), w - 1);
     // buffer resource over the readable rows (aligned base; OOB loads read 0)
     const uintptr_t pbase = reinterpret_cast<uintptr_t>(p.px);
     const uint32_t base_off = (uint32_t)(pbase & 3u);
@@ -137,13 +144,17 @@ __global__ __launch_bounds__(kThreads, DCTE_MIN_WAVES) void dcte_map(const MapPa
             tail |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, (int)(nrec4 + b), 0, 0) << (8u * b);
     }
 
-    uint32_t pref[G];
+    uint32_t pref[G][DPT];
     auto issue = [&](int g) {
 #pragma unroll
         for (int u = 0; u < G; u++) {
             int i = g * G + u;
             uint32_t a = row_start(i < n_in ? i : n_in - 1) & ~3u;
-            pref[u] = (tx < NDW) ? __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * tx), 0, 0) : 0u;
+#pragma unroll
+            for (int q = 0; q < DPT; q++) {
+                const int dw = tx + q * kThreads;
+                pref[u][q] = (dw < NDW) ? __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * dw), 0, 0) : 0u;
+            }
         }
     };
 
@@ -176,16 +187,20 @@ __global__ __launch_bounds__(kThreads, DCTE_MIN_WAVES) void dcte_map(const MapPa
     issue(0);
     for (int g = 0; g < ngroups; g++) {
         // stage raw bytes of group g, then prefetch group g + 1
-        if (tx < NDW) {
 #pragma unroll
-            for (int u = 0; u < G; u++) {
-                uint32_t v = pref[u];
-                if (tail_wg) {                     // uniform; a handful of WGs
-                    int i = g * G + u;
-                    uint32_t a = (row_start(i < n_in ? i : n_in - 1) & ~3u) + 4u * tx;
-                    if (a == nrec4) v = tail;
+        for (int q = 0; q < DPT; q++) {
+            const int dw = tx + q * kThreads;
+            if (dw < NDW) {
+#pragma unroll
+                for (int u = 0; u < G; u++) {
+                    uint32_t v = pref[u][q];
+                    if (tail_wg) {                 // uniform; a handful of WGs
+                        int i = g * G + u;
+                        uint32_t a = (row_start(i < n_in ? i : n_in - 1) & ~3u) + 4u * dw;
+                        if (a == nrec4) v = tail;
+                    }
+                    raw[u][dw] = v;
                 }
-                raw[u][tx] = v;
             }
         }
         if (g + 1 < ngroups) issue(g + 1);
@@ -199,17 +214,19 @@ __global__ __launch_bounds__(kThreads, DCTE_MIN_WAVES) void dcte_map(const MapPa
                 uint32_t off = (rs & 3u) + (uint32_t)((xc - xs) * BPP);
                 const uint8_t* rb = reinterpret_cast<const uint8_t*>(&raw[u][0]);
                 uint32_t c0 = rb[off], c1 = 0, c2 = 0;
-                if constexpr (BPP == 3) {
+                if constexpr (BPP >= 3) {
                     c1 = rb[off + 1];
                     c2 = rb[off + 2];
                 }
                 int L;
-                if constexpr (BPP == 1) {
-                    L = kLumaGrey * (int)c0;
+                if constexpr (SEM == kSemLqr) {
+                    L = (BPP == 1) ? kLumaGrey * (int)c0
+                                   : kLumaR * (int)c0 + kLumaG * (int)c1 + kLumaB * (int)c2;
+                    L -= kLumaBias;
                 } else {
-                    L = kLumaR * (int)c0 + kLumaG * (int)c1 + kLumaB * (int)c2;
+                    L = (int)preview_luma(c0, c1, c2, BPP) - kPreviewBias;
                 }
-                lum[u][cc] = (float)(L - kLumaBias);
+                lum[u][cc] = (float)L;
             }
         }
         __syncthreads();
@@ -257,24 +274,30 @@ __global__ __launch_bounds__(kThreads, DCTE_MIN_WAVES) void dcte_map(const MapPa
 // linear index k1*N + k2 with |C| == M (that is what "max <= currval" keeps).
 constexpr int kFixWaves = 4;
 
-template <int N>
+template <int N, int SEM>
 __global__ __launch_bounds__(64 * kFixWaves) void dcte_fix(const FixParams p)
 {
     __shared__ double win[kFixWaves][N * N];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     double* d = win[wv];
     const unsigned cnt = min(*p.fix_count, p.fix_cap);
-    constexpr int r = N / 2;
+    constexpr int HL = Geo<N, SEM>::HL;
     for (unsigned k = blockIdx.x * kFixWaves + wv; k < cnt; k += gridDim.x * kFixWaves) {
         const unsigned idx = p.fix_list[k];
         const int y = p.y0 + (int)(idx / (unsigned)p.w);
         const int x = (int)(idx % (unsigned)p.w);
         for (int e = lane; e < N * N; e += 64) {
-            const int i = e / N, j = e % N;          // d[i][j], i = x offset
-            const int xx = clampi(x + i - (r - 1), 0, p.w - 1);
-            const int yy = clampi(y + j - (r - 1), 0, p.h - 1);
+            // liblqr callback: data[dx][dy] (src/render.c:150);
+            // preview: data[dy][dx] (src/render.c:49)
+            const int i = e / N, j = e % N;
+            const int ox = SEM == kSemLqr ? i : j, oy = SEM == kSemLqr ? j : i;
+            const int xx = clampi(x + ox - HL, 0, p.w - 1);
+            const int yy = clampi(y + oy - HL, 0, p.h - 1);
             const uint8_t* px = p.px + (long long)(yy - p.in_row0) * p.rowstride + (long long)xx * p.bpp;
-            d[e] = r64::luma(px, p.bpp);
+            if constexpr (SEM == kSemLqr)
+                d[e] = r64::luma(px, p.bpp);
+            else
+                d[e] = (double)preview_luma(px[0], p.bpp > 1 ? px[1] : 0u, p.bpp > 1 ? px[2] : 0u, p.bpp);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -333,41 +356,61 @@ __global__ __launch_bounds__(64 * kFixWaves) void dcte_fix(const FixParams p)
 }
 
 // ------------------------------------------------------------------ launchers
-int map_tile_w(int n) { return n == 16 ? Geo<16>::TW : kThreads; }
+int map_tile_w(int n) { return n == 16 ? Geo<16, kSemLqr>::TW : kThreads; }
 int map_default_tile_h(int n) { return n == 16 ? DCTE_TILE_H16 : DCTE_TILE_H; }
 
-template <int N, int BPP>
+template <int N, int BPP, int SEM>
 static hipError_t launch_map_t(const MapParams& p, hipStream_t s)
 {
-    dim3 grid((p.w + Geo<N>::TW - 1) / Geo<N>::TW, (p.y1 - p.y0 + p.tile_h - 1) / p.tile_h);
-    hipLaunchKernelGGL((dcte_map<N, BPP>), grid, dim3(kThreads), 0, s, p);
+    constexpr int TW = Geo<N, SEM>::TW;
+    dim3 grid((p.w + TW - 1) / TW, (p.y1 - p.y0 + p.tile_h - 1) / p.tile_h);
+    hipLaunchKernelGGL((dcte_map<N, BPP, SEM>), grid, dim3(kThreads), 0, s, p);
     return hipGetLastError();
 }
 
-hipError_t launch_map(int n, int bpp, const MapParams& p, hipStream_t s)
+template <int N>
+static hipError_t launch_map_n(int bpp, int sem, const MapParams& p, hipStream_t s)
+{
+    if (sem == kSemLqr) {
+        if (bpp == 1) return launch_map_t<N, 1, kSemLqr>(p, s);
+        if (bpp == 3) return launch_map_t<N, 3, kSemLqr>(p, s);
+    } else if (sem == kSemPreview) {
+        if (bpp == 1) return launch_map_t<N, 1, kSemPreview>(p, s);
+        if (bpp == 3) return launch_map_t<N, 3, kSemPreview>(p, s);
+        if (bpp == 4) return launch_map_t<N, 4, kSemPreview>(p, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_map(int n, int bpp, int sem, const MapParams& p, hipStream_t s)
 {
     if (p.y1 <= p.y0) return hipSuccess;
-#define DCTE_CASE(NN)                                                          \
-    case NN:                                                                   \
-        return bpp == 1 ? launch_map_t<NN, 1>(p, s) : launch_map_t<NN, 3>(p, s);
     switch (n) {
-        DCTE_CASE(2)
-        DCTE_CASE(4)
-        DCTE_CASE(8)
-        DCTE_CASE(16)
+    case 2: return launch_map_n<2>(bpp, sem, p, s);
+    case 4: return launch_map_n<4>(bpp, sem, p, s);
+    case 8: return launch_map_n<8>(bpp, sem, p, s);
+    case 16: return launch_map_n<16>(bpp, sem, p, s);
     default: return hipErrorInvalidValue;
     }
-#undef DCTE_CASE
+}
+
+template <int N>
+static void launch_fix_n(const FixParams& p, hipStream_t s)
+{
+    dim3 grid(256), block(64 * kFixWaves);
+    if (p.sem == kSemLqr)
+        hipLaunchKernelGGL((dcte_fix<N, kSemLqr>), grid, block, 0, s, p);
+    else
+        hipLaunchKernelGGL((dcte_fix<N, kSemPreview>), grid, block, 0, s, p);
 }
 
 hipError_t launch_fix(const FixParams& p, hipStream_t s)
 {
-    dim3 grid(256), block(64 * kFixWaves);
     switch (p.n) {
-    case 2: hipLaunchKernelGGL(dcte_fix<2>, grid, block, 0, s, p); break;
-    case 4: hipLaunchKernelGGL(dcte_fix<4>, grid, block, 0, s, p); break;
-    case 8: hipLaunchKernelGGL(dcte_fix<8>, grid, block, 0, s, p); break;
-    case 16: hipLaunchKernelGGL(dcte_fix<16>, grid, block, 0, s, p); break;
+    case 2: launch_fix_n<2>(p, s); break;
+    case 4: launch_fix_n<4>(p, s); break;
+    case 8: launch_fix_n<8>(p, s); break;
+    case 16: launch_fix_n<16>(p, s); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

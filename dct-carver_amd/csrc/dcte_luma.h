@@ -11,7 +11,28 @@
 // which the energy never looks at (src/dct.c:119, "k1 || k2").
 #pragma once
 
+#if defined(__HIPCC__)
+#define DCTE_LUMA_HD __host__ __device__ __forceinline__
+#else
+#define DCTE_LUMA_HD static inline
+#endif
+
 namespace dcte {
+
+// energy semantics (DCTE_LQR / DCTE_PREVIEW in include/dctenergy.h)
+constexpr int kSemLqr = 0;
+constexpr int kSemPreview = 1;
+
+// Preview semantics: convert_row_to_luminance (src/render.c:62-79) with
+// RGB2LUMINANCE (src/render.h:5), evaluated in double left to right (the TU
+// is compiled without contraction) and truncated to guchar; grey copies the
+// byte.  The kernels work on L - 128, exact in fp32.
+constexpr int kPreviewBias = 128;
+DCTE_LUMA_HD unsigned preview_luma(unsigned r, unsigned g, unsigned b, int bpp)
+{
+    if (bpp == 1) return r;
+    return (unsigned char)(16.0 + r * 0.2568 + g * 0.5041 + b * 0.0979);
+}
 
 constexpr int kLumaR = 1063, kLumaG = 3576, kLumaB = 361, kLumaGrey = 5000;
 constexpr int kLumaBias = 637500;

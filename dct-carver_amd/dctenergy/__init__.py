@@ -87,7 +87,7 @@ def lib():
     L.dcte_energy_map_device.argtypes = [vp, ctypes.c_int, vp, ctypes.c_longlong, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
-                                         ctypes.c_float, vp, ctypes.c_longlong, vp]
+                                         ctypes.c_float, ctypes.c_int, vp, ctypes.c_longlong, vp]
     L.dcte_last_refined.restype = ctypes.c_longlong
     L.dcte_last_refined.argtypes = [vp]
     L.dcte_profile_read.restype = ctypes.c_int
@@ -98,7 +98,8 @@ def lib():
     L.dcte_energy_image_u8.restype = ctypes.c_int
     L.dcte_energy_image_u8.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_size_t, ctypes.c_int, ctypes.c_float,
-                                       ctypes.c_float, ctypes.c_int, ctypes.c_int, vp]
+                                       ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       vp]
     L.dcte_minmax_device.restype = ctypes.c_int
     L.dcte_minmax_device.argtypes = [vp, ctypes.c_int, vp, ctypes.c_longlong, vp, vp]
     L.dcte_normalize_u8_device.restype = ctypes.c_int
@@ -204,13 +205,14 @@ class Context:
                                             out.ctypes.data))
         return out
 
-    def energy_image_u8(self, px, n=8, edges=0.5, textures=0.5, mode=DCTE_NORM_LQR, channels=1):
+    def energy_image_u8(self, px, n=8, edges=0.5, textures=0.5, mode=DCTE_NORM_LQR, channels=1,
+                        semantics=DCTE_LQR):
         px = np.ascontiguousarray(px, dtype=np.uint8)
         h, w = px.shape[:2]
         bpp = 1 if px.ndim == 2 else px.shape[2]
         out = np.empty((h, w) + ((channels,) if channels > 1 else ()), np.uint8)
         self._check(lib().dcte_energy_image_u8(self._h, px.ctypes.data, w, h, bpp, px.strides[0],
-                                               n, edges, textures, mode, channels,
+                                               n, edges, textures, semantics, mode, channels,
                                                out.ctypes.data))
         return out
 
@@ -226,14 +228,15 @@ class Context:
 
     # -- device entry point (HBM-resident frames; addresses as ints)
     def energy_map_device(self, d_px, rowstride, w, h, bpp, in_row0, in_rows, y0, y1, n,
-                          edges, textures, d_out, out_stride, stream=0, device=0):
+                          edges, textures, d_out, out_stride, stream=0, device=0,
+                          semantics=DCTE_LQR):
         self._check(lib().dcte_energy_map_device(
             self._h, device, ctypes.c_void_p(d_px), rowstride, w, h, bpp, in_row0, in_rows,
-            y0, y1, n, edges, textures, ctypes.c_void_p(d_out), out_stride,
+            y0, y1, n, edges, textures, semantics, ctypes.c_void_p(d_out), out_stride,
             ctypes.c_void_p(stream)))
 
     def energy_map_tensor(self, px, out, n=8, edges=0.5, textures=0.5, h=None, in_row0=0,
-                          y0=None, y1=None, stream=None, device=0):
+                          y0=None, y1=None, stream=None, device=0, semantics=DCTE_LQR):
         """torch.uint8 CUDA frame rows (HxW or HxWxC; row 0 = global row
         `in_row0` of an image of height `h`) -> rows [y0, y1) into `out`."""
         import torch  # plumbing only: device memory and the current stream
@@ -253,7 +256,8 @@ class Context:
         if stream is None:
             stream = torch.cuda.current_stream(px.device).cuda_stream
         self.energy_map_device(px.data_ptr(), px.stride(0), w, h, bpp, in_row0, rows, y0, y1,
-                               n, edges, textures, out.data_ptr(), out.stride(0), stream, device)
+                               n, edges, textures, out.data_ptr(), out.stride(0), stream, device,
+                               semantics)
         return out
 
 

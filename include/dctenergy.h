@@ -54,9 +54,17 @@ extern "C" {
 #define DCTE_ERANGE (-5)   /* frame too large for one launch (> 4 GiB band) */
 #define DCTE_ENOTSUP (-6)  /* recognised but not provided by this build */
 
-/* energy semantics */
-#define DCTE_LQR 0         /* liblqr callback semantics, src/render.c:134-157 */
-#define DCTE_PREVIEW 1     /* GTK preview semantics, src/render.c:31-109 */
+/* energy semantics
+ * DCTE_LQR     the liblqr energy callback dct_pixel_energy (src/render.c:134-157):
+ *              liblqr luma [unverified] in [0,1], window -(N/2-1)..N/2,
+ *              bpp 1 or 3 (alpha handling is liblqr's and unverifiable here)
+ * DCTE_PREVIEW the dialog preview dct_energy_preview (src/render.c:31-79,
+ *              421-479): u8 luma RGB2LUMINANCE (src/render.h:5; grey = the
+ *              byte), window -(c-1)..N-c with c = (N-1)/2 (src/dct.h:8-9),
+ *              clamp to the region passed in; bpp 1, 3 or 4 (alpha ignored,
+ *              as convert_row_to_luminance does) */
+#define DCTE_LQR 0
+#define DCTE_PREVIEW 1
 
 /* options for dcte_set_option */
 #define DCTE_OPT_TIE_TAU 1 /* relative edge/texture margin refined in fp64
@@ -88,7 +96,7 @@ int dcte_set_option(dcte_ctx *ctx, int option, double value);
  *             lqr_carver_new, src/render.c:159-173,312)
  *   n         blocksize N (2, 4, 8, 16)
  *   edges, textures   weights (PlugInVals, src/main.h:12-22)
- *   semantics DCTE_LQR
+ *   semantics DCTE_LQR or DCTE_PREVIEW
  *   transposed 0 (1 = map of the transposed frame; not in this build)
  *   out       caller-owned w*h floats, row-major
  * With several devices the frame is split into row bands; each device
@@ -108,7 +116,7 @@ int dcte_energy_map(dcte_ctx *ctx, const uint8_t *px, int w, int h, int bpp,
 int dcte_energy_map_device(dcte_ctx *ctx, int device, const void *d_px,
                            long long rowstride, int w, int h, int bpp,
                            int in_row0, int in_rows, int y0, int y1, int n,
-                           float edges, float textures, float *d_out,
+                           float edges, float textures, int semantics, float *d_out,
                            long long out_stride, void *stream);
 
 /* ---- energy image as 8-bit grey ----------------------
@@ -130,7 +138,7 @@ int dcte_normalize_u8(dcte_ctx *ctx, const float *E, size_t n, int mode, int cha
  * w*h*channels bytes.  Several devices: band maps, one global min/max. */
 int dcte_energy_image_u8(dcte_ctx *ctx, const uint8_t *px, int w, int h, int bpp,
                          size_t rowstride, int n, float edges, float textures,
-                         int mode, int channels, uint8_t *out);
+                         int semantics, int mode, int channels, uint8_t *out);
 
 /* device pieces (stream-ordered, no sync): min/max of n floats into
  * d_minmax[0..1]; then normalise with a (possibly all-reduced) d_minmax */

@@ -25,6 +25,12 @@
  *                 cftx020 :3211, dctsub :3274, makect :724 (N=2,4 only)
  *   weighted max  src/dct.c:112-126 (weighted_max_dct_correlation) with the
  *                 edge-atom LUTs src/dct.c:26-59 (edges = (0,1),(1,0))
+ *   preview       the GTK preview's second energy semantics,
+ *                 dct_energy_preview / dct_energy_preview_rows /
+ *                 convert_row_to_luminance (src/render.c:31-79, :421-479):
+ *                 u8 luma RGB2LUMINANCE (src/render.h:5), window rows and
+ *                 columns -(c-1)..N-c with c = CENTER_ROW(N) = (N-1)/2
+ *                 (src/dct.h:8-9), stored data[dy][dx]
  *
  * Compile with -ffp-contract=off (the Makefile does): the reference is plain
  * C on x86-64 where gcc emits no fused multiply-adds.
@@ -333,6 +339,55 @@ int orc_energy_map(const uint8_t *px, int w, int h, int bpp, size_t rowstride, i
 {
     return orc_energy_map_rows(px, w, h, bpp, rowstride, n, edges, textures, 0, h,
                                nthreads, out);
+}
+
+/* ---- preview semantics (src/render.c:31-79, 421-479) ------------------- */
+
+/* convert_row_to_luminance (src/render.c:62-79): grey copies the byte; 3 or
+ * more channels use RGB2LUMINANCE (src/render.h:5), evaluated in double left
+ * to right and truncated to guchar; 2 channels are rejected (the reference
+ * reports an error and leaves the row unconverted). */
+uint8_t orc_preview_luma(const uint8_t *p, int bpp)
+{
+    if (bpp == 1) return p[0];
+    return (uint8_t)(16.0 + p[0] * 0.2568 + p[1] * 0.5041 + p[2] * 0.0979);
+}
+
+/* Preview energies (before normalize_image) of a w x h region, rows
+ * [y0, y1) into out[(y - y0) * w + x]; px addresses the region's row 0. */
+int orc_preview_map_rows(const uint8_t *px, int w, int h, int bpp, size_t rowstride, int n,
+                         float edges, float textures, int y0, int y1, int nthreads, float *out)
+{
+    if (bpp != 1 && bpp != 3 && bpp != 4) return -1;
+    if (!valid_n(n) || w <= 0 || h <= 0 || y0 < 0 || y1 > h || y0 > y1) return -1;
+    const int c = (n - 1) / 2; /* CENTER_ROW / CENTER_COL */
+    uint8_t *L = (uint8_t *)malloc((size_t)w * h);
+    if (!L) return -2;
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++)
+            L[(size_t)y * w + x] = orc_preview_luma(px + (size_t)y * rowstride + (size_t)x * bpp, bpp);
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+#endif
+    for (int y = y0; y < y1; y++) {
+        double d[256];
+        for (int x = 0; x < w; x++) {
+            for (int ii = 0; ii < n; ii++) {            /* data[dy][dx] */
+                int yy = y + ii - (c - 1);
+                yy = yy < 0 ? 0 : (yy > h - 1 ? h - 1 : yy);
+                for (int jj = 0; jj < n; jj++) {
+                    int xx = x + jj - (c - 1);
+                    xx = xx < 0 ? 0 : (xx > w - 1 ? w - 1 : xx);
+                    d[ii * n + jj] = L[(size_t)yy * w + xx];
+                }
+            }
+            orc_dct(n, d);
+            out[(size_t)(y - y0) * w + x] = orc_weighted_max(n, d, edges, textures);
+        }
+    }
+    free(L);
+    return 0;
 }
 
 int orc_max_threads(void)

@@ -15,6 +15,8 @@
  *   - dctNxN dispatch           src/dct.c:93-110
  *   - weighted max + edge LUT   src/dct.c:72-89, 112-126
  *   - window gather + clamp     src/render.c:122-157
+ *   - preview gather + luma     src/render.c:31-79 (row-streamed window over
+ *                               u8 luma rows, RGB2LUMINANCE src/render.h:5)
  * Everything numeric (ddct8x8s, ddct16x16s, ddct2d) is the reference's code.
  */
 #include <math.h>
@@ -140,5 +142,51 @@ int ref_energy_map_luma(const double *luma, int w, int h, int n, float edges,
             out[(size_t)y * w + x] = weighted_max(&s, edges, textures);
         }
     scratch_free(&s);
+    return 0;
+}
+
+/* Preview semantics (src/render.c:31-79, 421-479): the row-streamed window of
+ * dct_energy_preview over u8 luma rows, one scratch per row as the reference
+ * allocates it (src/render.c:37-41), reference transforms. */
+int ref_preview_map(const uint8_t *px, int w, int h, int bpp, int n, float edges,
+                    float textures, float *out)
+{
+    if (n != 2 && n != 4 && n != 8 && n != 16) return -1;
+    if (bpp != 1 && bpp != 3 && bpp != 4) return -1;
+    int c = (n - 1) / 2;
+    unsigned char *L = (unsigned char *)malloc((size_t)w * h);
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            const uint8_t *q = px + ((size_t)y * w + x) * bpp;
+            L[(size_t)y * w + x] = bpp == 1 ? q[0]
+                : (unsigned char)(16.0 + (q[0]) * 0.2568 + (q[1]) * 0.5041 + (q[2]) * 0.0979);
+        }
+    const unsigned char **rows = (const unsigned char **)malloc(sizeof(*rows) * n);
+    for (int i = 0; i < n; i++) {                 /* initial fill, src/render.c:459-463 */
+        int r0 = i - (c - 1);
+        r0 = r0 < 0 ? 0 : (r0 > h - 1 ? h - 1 : r0);
+        rows[i] = L + (size_t)r0 * w;
+    }
+    for (int y = 0; y < h; y++) {
+        ref_scratch s;
+        scratch_init(&s, n);
+        for (int j = 0; j < w; j++) {             /* dct_energy_preview_rows */
+            int left = j - (c - 1), right = j + n - c;
+            for (int ii = 0; ii < n; ii++)
+                for (int jj = left; jj <= right; jj++) {
+                    int cj = jj < 0 ? 0 : (jj > w - 1 ? w - 1 : jj);
+                    s.data[ii][jj - left] = rows[ii][cj];
+                }
+            dispatch(&s);
+            out[(size_t)y * w + j] = weighted_max(&s, edges, textures);
+        }
+        scratch_free(&s);
+        /* shuffle rows, append MIN(y + n - (c - 1), h - 1) (src/render.c:467-475) */
+        for (int i = 1; i < n; i++) rows[i - 1] = rows[i];
+        int nr = y + n - (c - 1);
+        rows[n - 1] = L + (size_t)(nr < h - 1 ? nr : h - 1) * w;
+    }
+    free(rows);
+    free(L);
     return 0;
 }

@@ -24,32 +24,33 @@ def lib():
         L.emu_energy_map.restype = ctypes.c_int
         L.emu_energy_map.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_size_t, ctypes.c_int, ctypes.c_float,
-                                     ctypes.c_float, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      _f32p, _f32p, _f32p]
         _lib = L
     return _lib
 
 
-def scale(n):
-    return LUMA_SCALE * (n if n >= 8 else 1)
+def scale(n, sem=0):
+    return (LUMA_SCALE if sem == 0 else 1.0) * (n if n >= 8 else 1)
 
 
-def kernel_weights(n, edges, textures):
+def kernel_weights(n, edges, textures, sem=0):
     """The launcher's pre-scaled weights (dcte_capi.cpp run_device)."""
-    s = scale(n)
+    s = scale(n, sem)
     return np.float32(np.float64(np.float32(edges)) / s), np.float32(np.float64(np.float32(textures)) / s)
 
 
-def energy_map(img, n, edges, textures):
-    """-> (E_fast, m_e, m_t), exactly the kernel's fast-path values."""
+def energy_map(img, n, edges, textures, sem=0):
+    """-> (E_fast, m_e, m_t), exactly the kernel's fast-path values
+    (sem 0 = liblqr callback semantics, 1 = preview semantics)."""
     img = np.ascontiguousarray(img, dtype=np.uint8)
     h, w = img.shape[:2]
     bpp = 1 if img.ndim == 2 else img.shape[2]
-    we, wt = kernel_weights(n, edges, textures)
+    we, wt = kernel_weights(n, edges, textures, sem)
     E = np.empty((h, w), np.float32)
     me = np.empty_like(E)
     mt = np.empty_like(E)
-    rc = lib().emu_energy_map(img.ctypes.data_as(_u8p), w, h, bpp, w * bpp, n, we, wt, 0, h,
+    rc = lib().emu_energy_map(img.ctypes.data_as(_u8p), w, h, bpp, w * bpp, n, we, wt, sem, 0, h,
                               E.ctypes.data_as(_f32p), me.ctypes.data_as(_f32p),
                               mt.ctypes.data_as(_f32p))
     assert rc == 0

@@ -138,6 +138,35 @@ def main():
         for n in (2, 4, 8, 16):
             add_map(name, inputs[name], n, 0.15, 0.85)
 
+    # preview semantics (src/render.c:31-109): float energies from the
+    # reference transforms over the restated row streaming, plus the u8
+    # image normalize_image would draw (numpy restatement, tests/oracle_py.py)
+    manifest["preview"] = []
+    rng = np.random.default_rng(21)
+    prev_inputs = {
+        "natural_rgb_73x59": inputs["natural_rgb_73x59"],
+        "natural_grey_200x120": inputs["natural_grey_200x120"],
+        "rgba_45x38": np.concatenate([natural(38, 45, 3, 5), rng.integers(0, 256, (38, 45, 1), dtype=np.uint8)], -1),
+        "uniform_rgb_57x63": inputs["uniform_rgb_57x63"],
+        "tiny_grey_2x3": inputs["tiny_grey_2x3"],
+        "tiny_rgb_1x1": inputs["tiny_rgb_1x1"],
+    }
+    if "wilber_rgb_74x59" in inputs:
+        prev_inputs["wilber_rgb_74x59"] = inputs["wilber_rgb_74x59"]
+    np.save(os.path.join(HERE, "inputs", "rgba_45x38.npy"), prev_inputs["rgba_45x38"])
+    for name, img in prev_inputs.items():
+        for n in (2, 4, 8, 16):
+            for e, t in ((0.5, 0.5), (0.15, 0.85)):
+                E = O.ref_preview_map(img, n, e, t)
+                ofile = f"preview__{name}__n{n}_e{e}_t{t}.npy"
+                np.save(os.path.join(HERE, "maps", ofile), E)
+                ch = 1 if img.ndim == 2 else img.shape[2]
+                u8file = ofile.replace(".npy", "_u8.npy")
+                np.save(os.path.join(HERE, "maps", u8file), O.normalize_preview(E, ch))
+                manifest["preview"].append({"input": f"{name}.npy", "output": ofile,
+                                            "output_u8": u8file, "N": n, "edges": e,
+                                            "textures": t, "channels": ch})
+
     kats = kat_windows()
     os.makedirs(os.path.join(HERE, "kat"), exist_ok=True)
     for name, win in kats.items():
@@ -148,7 +177,8 @@ def main():
 
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1)
-    print(len(manifest["maps"]), "maps,", len(manifest["kat"]), "KAT entries")
+    print(len(manifest["maps"]), "maps,", len(manifest["preview"]), "preview maps,",
+          len(manifest["kat"]), "KAT entries")
 
 
 if __name__ == "__main__":

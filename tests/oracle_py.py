@@ -55,6 +55,13 @@ def lib():
         L.orc_luma.restype = ctypes.c_double
         L.orc_luma.argtypes = [_u8p, ctypes.c_int]
         L.orc_max_threads.restype = ctypes.c_int
+        L.orc_preview_luma.restype = ctypes.c_uint8
+        L.orc_preview_luma.argtypes = [_u8p, ctypes.c_int]
+        L.orc_preview_map_rows.restype = ctypes.c_int
+        L.orc_preview_map_rows.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_size_t, ctypes.c_int, ctypes.c_float,
+                                           ctypes.c_float, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, _f32p]
         _lib = L
     return _lib
 
@@ -74,6 +81,9 @@ def ref():
                                           ctypes.c_float, ctypes.c_float, _f32p]
         R.ref_window_energy.restype = ctypes.c_float
         R.ref_window_energy.argtypes = [ctypes.c_int, _f64p, ctypes.c_float, ctypes.c_float]
+        R.ref_preview_map.restype = ctypes.c_int
+        R.ref_preview_map.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_int, ctypes.c_float, ctypes.c_float, _f32p]
         R.ref_dct.restype = ctypes.c_int
         R.ref_dct.argtypes = [ctypes.c_int, _f64p]
         _ref = R
@@ -102,6 +112,21 @@ def energy_map_luma(luma, n, edges, textures, nthreads=1):
     out = np.empty((h, w), np.float32)
     rc = lib().orc_energy_map_luma_rows(_ptr(luma, _f64p), 0, h, w, h, n, edges, textures,
                                         0, h, nthreads, _ptr(out, _f32p))
+    if rc != 0:
+        raise ValueError(f"oracle rejected the call (rc={rc})")
+    return out
+
+
+def preview_map(px, n, edges, textures, y0=0, y1=None, nthreads=1):
+    """Preview-semantics energies (src/render.c:31-79) of an HxW / HxWxC region."""
+    px = np.ascontiguousarray(px, dtype=np.uint8)
+    h, w = px.shape[:2]
+    bpp = 1 if px.ndim == 2 else px.shape[2]
+    if y1 is None:
+        y1 = h
+    out = np.empty((y1 - y0, w), np.float32)
+    rc = lib().orc_preview_map_rows(_ptr(px, _u8p), w, h, bpp, w * bpp, n, edges, textures,
+                                    y0, y1, nthreads, _ptr(out, _f32p))
     if rc != 0:
         raise ValueError(f"oracle rejected the call (rc={rc})")
     return out
@@ -138,6 +163,17 @@ def ref_energy_map_luma(luma, n, edges, textures):
     h, w = luma.shape
     out = np.empty((h, w), np.float32)
     rc = R.ref_energy_map_luma(_ptr(luma, _f64p), w, h, n, edges, textures, _ptr(out, _f32p))
+    if rc != 0:
+        raise ValueError("reference rejected the call")
+    return out
+
+
+def ref_preview_map(px, n, edges, textures):
+    px = np.ascontiguousarray(px, dtype=np.uint8)
+    h, w = px.shape[:2]
+    bpp = 1 if px.ndim == 2 else px.shape[2]
+    out = np.empty((h, w), np.float32)
+    rc = ref().ref_preview_map(_ptr(px, _u8p), w, h, bpp, n, edges, textures, _ptr(out, _f32p))
     if rc != 0:
         raise ValueError("reference rejected the call")
     return out

@@ -84,3 +84,14 @@ def test_fp32_error_bound_vs_max_coefficient(n):
         m = np.maximum(np.maximum(me_r, mt_r), 1e-12)
         assert (np.abs(me / s - me_r) / m).max() < 2e-6
         assert (np.abs(mt / s - mt_r) / m).max() < 2e-6
+
+
+@pytest.mark.parametrize("entry", manifest()["preview"], ids=lambda e: e["output"])
+def test_emulated_kernel_vs_golden_preview(entry):
+    """Preview semantics (src/render.c:31-79) through the kernel's arithmetic."""
+    img = load_input(entry["input"])
+    ref = load_map(entry["output"])
+    E, me, mt = EM.energy_map(img, entry["N"], entry["edges"], entry["textures"], sem=1)
+    refine = EM.refine_mask(me, mt, entry["edges"], entry["textures"])
+    ok = np.abs(E.astype(np.float64) - ref) <= RTOL * np.abs(ref.astype(np.float64)) + ATOL
+    assert not (~ok & ~refine).any()

@@ -94,7 +94,7 @@ def test_bad_arguments(ctx):
         ctx.energy_map(np.zeros((16, 16, 2), np.uint8), 8)
     assert ei.value.code == dctenergy.DCTE_EINVAL
     with pytest.raises(dctenergy.DcteError) as ei:
-        ctx.energy_map(img, 8, semantics=dctenergy.DCTE_PREVIEW)
+        ctx.energy_map(img, 8, transposed=True)
     assert ei.value.code == dctenergy.DCTE_ENOTSUP
 
 
@@ -235,3 +235,46 @@ def test_energy_image_u8_fused(ctx):
     assert np.array_equal(u8, O.normalize_lqr(E))
     u8p = ctx.energy_image_u8(img, 8, 0.3, 0.7, dctenergy.DCTE_NORM_PREVIEW, 3)
     assert np.array_equal(u8p, O.normalize_preview(E, 3))
+
+
+@pytest.mark.parametrize("entry", manifest()["preview"], ids=lambda e: e["output"])
+def test_preview_golden(ctx, entry):
+    """Preview semantics (src/render.c:31-109) on the GPU: float energies within
+    tolerance, the u8 image equal to normalize_image of them."""
+    img = load_input(entry["input"])
+    E = ctx.energy_map(img, entry["N"], entry["edges"], entry["textures"],
+                       semantics=dctenergy.DCTE_PREVIEW)
+    _assert_tol(E, load_map(entry["output"]), entry["output"])
+    u8 = ctx.energy_image_u8(img, entry["N"], entry["edges"], entry["textures"],
+                             dctenergy.DCTE_NORM_PREVIEW, entry["channels"],
+                             semantics=dctenergy.DCTE_PREVIEW)
+    assert np.array_equal(u8, O.normalize_preview(E, entry["channels"]))
+    gold = load_map(entry["output_u8"]).astype(np.int16)
+    assert np.abs(u8.astype(np.int16) - gold).max() <= 1
+
+
+def test_preview_refine_everything_is_bit_exact():
+    with dctenergy.Context(ngpus=1, tie_tau=1.0) as c:
+        for entry in manifest()["preview"]:
+            img = load_input(entry["input"])
+            got = c.energy_map(img, entry["N"], entry["edges"], entry["textures"],
+                               semantics=dctenergy.DCTE_PREVIEW)
+            assert np.array_equal(got, load_map(entry["output"])), entry["output"]
+
+
+def test_preview_fast_path_equals_emulation():
+    rng = np.random.default_rng(8)
+    imgs = [load_input("rgba_45x38.npy"), rng.integers(0, 256, (70, 301, 3), dtype=np.uint8),
+            rng.integers(0, 256, (33, 257), dtype=np.uint8)]
+    with dctenergy.Context(ngpus=1, tie_tau=0.0) as c:
+        for img in imgs:
+            for n in (2, 4, 8, 16):
+                got = c.energy_map(img, n, 0.3, 0.7, semantics=dctenergy.DCTE_PREVIEW)
+                E, _, _ = EM.energy_map(img, n, 0.3, 0.7, sem=1)
+                assert np.array_equal(got, E), (img.shape, n)
+
+
+def test_preview_rejects_two_channels(ctx):
+    with pytest.raises(dctenergy.DcteError) as ei:
+        ctx.energy_map(np.zeros((8, 8, 2), np.uint8), 8, semantics=dctenergy.DCTE_PREVIEW)
+    assert ei.value.code == dctenergy.DCTE_EINVAL

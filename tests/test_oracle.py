@@ -72,3 +72,19 @@ def test_oracle_map_vs_reference_random_images():
         img = rng.integers(0, 256, (37, 53, 3), dtype=np.uint8)
         L = O.luma_plane(img)
         assert np.array_equal(O.energy_map(img, n, 0.2, 0.8), O.ref_energy_map_luma(L, n, 0.2, 0.8))
+
+
+@pytest.mark.parametrize("entry", manifest()["preview"], ids=lambda e: e["output"])
+def test_oracle_preview_matches_golden(entry):
+    img = load_input(entry["input"])
+    got = O.preview_map(img, entry["N"], entry["edges"], entry["textures"])
+    assert np.array_equal(got, load_map(entry["output"]))
+    assert np.array_equal(O.normalize_preview(got, entry["channels"]), load_map(entry["output_u8"]))
+
+
+def test_preview_luma_is_the_macro():
+    """RGB2LUMINANCE (src/render.h:5) evaluated in double, truncated."""
+    for rgb in ((0, 0, 0), (255, 255, 255), (10, 200, 30), (255, 0, 128)):
+        px = np.array(rgb, np.uint8)
+        want = int(16.0 + rgb[0] * 0.2568 + rgb[1] * 0.5041 + rgb[2] * 0.0979)
+        assert O.lib().orc_preview_luma(px.ctypes.data_as(O._u8p), 3) == want

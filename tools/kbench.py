@@ -24,7 +24,7 @@ def load(path):
     L.dcte_energy_map_device.argtypes = [vp, ctypes.c_int, vp, ctypes.c_longlong, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
-                                         ctypes.c_float, vp, ctypes.c_longlong, vp]
+                                         ctypes.c_float, ctypes.c_int, vp, ctypes.c_longlong, vp]
     L.dcte_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
     h = vp()
     assert L.dcte_create(ctypes.byref(h), 1, 0) == 0
@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--bpp", type=int, default=3)
+    ap.add_argument("--sem", type=int, default=0)
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     import torch
@@ -55,7 +56,7 @@ def main():
         for p, L, h in libs:
             for _ in range(a.iters + 1):
                 rc = L.dcte_energy_map_device(h, 0, frame.data_ptr(), frame.stride(0), S, S, a.bpp, 0, S,
-                                              0, S, a.n, 0.3, 0.7, out.data_ptr(), out.stride(0), stream)
+                                              0, S, a.n, 0.3, 0.7, a.sem, out.data_ptr(), out.stride(0), stream)
                 assert rc == 0, rc
             n = ctypes.c_longlong()
             ms = ctypes.c_double()
