@@ -43,6 +43,8 @@ struct Device {
     float* d_minmax = nullptr;
     uint8_t* d_u8 = nullptr;       // u8 staging for the host entry points
     size_t u8_cap = 0;
+    uint8_t* d_tr = nullptr;       // transposed band (transposed maps)
+    size_t tr_cap = 0;
 };
 
 }  // namespace
@@ -245,29 +247,46 @@ bool valid_norm(int mode, int channels)
 }
 
 // host frame -> device band maps (rows split over the context's devices),
-// left on the devices in d.d_out; returns the number of devices used
+// left on the devices in d.d_out; returns the number of devices used.
+// transposed: the map of the transposed frame (w x h -> h x w); device k
+// takes a strip of source COLUMNS (= transposed rows) plus halo, transposes
+// it in HBM and maps it.
 int map_bands(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride, int n,
-              float edges, float textures, int sem, int* used)
+              float edges, float textures, int sem, int transposed, int* used)
 {
-    const int G = (int)ctx->devs.size() < h ? (int)ctx->devs.size() : h;
-    const size_t pitch = (size_t)w * bpp;
+    const int W = transposed ? h : w, H = transposed ? w : h;   // mapped frame
+    const int G = (int)ctx->devs.size() < H ? (int)ctx->devs.size() : H;
     for (int k = 0; k < G; k++) {
         Device& d = ctx->devs[k];
-        int y0 = (int)((long long)h * k / G), y1 = (int)((long long)h * (k + 1) / G);
+        int y0 = (int)((long long)H * k / G), y1 = (int)((long long)H * (k + 1) / G);
         int lo, hi;
-        needed_rows(n, sem, h, y0, y1, lo, hi);
+        needed_rows(n, sem, H, y0, y1, lo, hi);
+        const size_t pitch = (size_t)W * bpp;                   // mapped-frame row
         size_t in_bytes = pitch * (size_t)(hi - lo + 1);
-        size_t out_bytes = sizeof(float) * (size_t)w * (size_t)(y1 - y0);
+        size_t out_bytes = sizeof(float) * (size_t)W * (size_t)(y1 - y0);
         int rc = ensure_stream(ctx, d);
         if (rc) return rc;
         rc = ensure_buf(ctx, (void**)&d.d_in, &d.in_cap, in_bytes);
         if (rc) return rc;
         rc = ensure_buf(ctx, (void**)&d.d_out, &d.out_cap, out_bytes);
         if (rc) return rc;
-        DCTE_HIP(ctx, hipMemcpy2DAsync(d.d_in, pitch, px + (size_t)lo * rowstride, rowstride,
-                                       pitch, hi - lo + 1, hipMemcpyHostToDevice, d.stream));
-        rc = run_device(ctx, d, d.d_in, (long long)pitch, w, h, bpp, lo, hi - lo + 1, y0, y1, n,
-                        edges, textures, sem, d.d_out, w, d.stream);
+        const uint8_t* band = d.d_in;
+        if (!transposed) {
+            DCTE_HIP(ctx, hipMemcpy2DAsync(d.d_in, pitch, px + (size_t)lo * rowstride, rowstride,
+                                           pitch, hi - lo + 1, hipMemcpyHostToDevice, d.stream));
+        } else {
+            // source columns [lo, hi] of all h rows -> (h x cols) strip -> transpose
+            const size_t sw = (size_t)(hi - lo + 1) * bpp;
+            DCTE_HIP(ctx, hipMemcpy2DAsync(d.d_in, sw, px + (size_t)lo * bpp, rowstride, sw, h,
+                                           hipMemcpyHostToDevice, d.stream));
+            rc = ensure_buf(ctx, (void**)&d.d_tr, &d.tr_cap, in_bytes);
+            if (rc) return rc;
+            DCTE_HIP(ctx, dcte::launch_transpose_u8(d.d_in, (long long)sw, h, hi - lo + 1, bpp,
+                                                    d.d_tr, (long long)pitch, d.stream));
+            band = d.d_tr;
+        }
+        rc = run_device(ctx, d, band, (long long)pitch, W, H, bpp, lo, hi - lo + 1, y0, y1, n,
+                        edges, textures, sem, d.d_out, W, d.stream);
         if (rc) return rc;
     }
     *used = G;
@@ -337,6 +356,7 @@ void dcte_destroy(dcte_ctx* ctx)
         if (d.d_out) (void)hipFree(d.d_out);
         if (d.d_keys) (void)hipFree(d.d_keys);
         if (d.d_u8) (void)hipFree(d.d_u8);
+        if (d.d_tr) (void)hipFree(d.d_tr);
         if (d.stream) (void)hipStreamDestroy(d.stream);
     }
     delete ctx;
@@ -375,17 +395,17 @@ int dcte_energy_map(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, siz
     if (!ctx || !px || !out) return DCTE_EINVAL;
     if (!valid_n(n) || !valid_sem_bpp(semantics, bpp) || w <= 0 || h <= 0) return DCTE_EINVAL;
     if (rowstride < (size_t)w * bpp) return DCTE_EINVAL;
-    if (transposed) return DCTE_ENOTSUP;
     ctx->last_refined = 0;
     int G = 0;
-    int rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, &G);
+    int rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, transposed, &G);
     if (rc) return rc;
+    const int W = transposed ? h : w, H = transposed ? w : h;
     for (int k = 0; k < G; k++) {
         Device& d = ctx->devs[k];
-        int y0 = (int)((long long)h * k / G), y1 = (int)((long long)h * (k + 1) / G);
+        int y0 = (int)((long long)H * k / G), y1 = (int)((long long)H * (k + 1) / G);
         DCTE_HIP(ctx, hipSetDevice(d.id));
-        DCTE_HIP(ctx, hipMemcpyAsync(out + (size_t)y0 * w, d.d_out,
-                                     sizeof(float) * (size_t)w * (size_t)(y1 - y0),
+        DCTE_HIP(ctx, hipMemcpyAsync(out + (size_t)y0 * W, d.d_out,
+                                     sizeof(float) * (size_t)W * (size_t)(y1 - y0),
                                      hipMemcpyDeviceToHost, d.stream));
     }
     return sync_bands(ctx, G);
@@ -400,7 +420,7 @@ int dcte_energy_image_u8(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp
     if (rowstride < (size_t)w * bpp || !valid_norm(mode, channels)) return DCTE_EINVAL;
     ctx->last_refined = 0;
     int G = 0;
-    int rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, &G);
+    int rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, 0, &G);
     if (rc) return rc;
     // per-band min/max, reduced on the host (2 floats per device)
     float gmin = 0, gmax = 0;

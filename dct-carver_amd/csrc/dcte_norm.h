@@ -15,4 +15,8 @@ hipError_t launch_minmax(const float* e, long long n, unsigned* keys, float* min
 hipError_t launch_to_u8(const float* e, long long n, const float* minmax, int mode, int channels,
                         uint8_t* out, hipStream_t s);
 
+// u8 frame (rows x cols x bpp) -> its transpose (cols x rows x bpp)
+hipError_t launch_transpose_u8(const uint8_t* src, long long src_pitch, int rows, int cols, int bpp,
+                               uint8_t* dst, long long dst_pitch, hipStream_t s);
+
 }  // namespace dcte

@@ -128,3 +128,46 @@ hipError_t launch_to_u8(const float* e, long long n, const float* minmax, int mo
 }
 
 }  // namespace dcte
+
+namespace dcte {
+
+// ------------------------------------------------------------------ transpose
+// u8 interleaved frame (rows x cols x bpp, pitch src_pitch bytes) ->
+// its transpose (cols x rows x bpp, pitch dst_pitch), through 64x64 LDS tiles.
+template <int BPP>
+__global__ __launch_bounds__(256) void dcte_transpose_u8(const uint8_t* __restrict__ src,
+                                                        long long src_pitch, int rows, int cols,
+                                                        uint8_t* __restrict__ dst,
+                                                        long long dst_pitch)
+{
+    __shared__ uint8_t tile[64][64 * BPP + 4];
+    const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+    for (int i = threadIdx.x; i < 64 * 64 * BPP; i += 256) {
+        const int rr = i / (64 * BPP), cb = i % (64 * BPP);
+        const int r = r0 + rr, cbyte = c0 * BPP + cb;
+        if (r < rows && cbyte < cols * BPP) tile[rr][cb] = src[(long long)r * src_pitch + cbyte];
+    }
+    __syncthreads();
+    // dst row = source column c0 + cc, dst column = source row r0 + rr
+    for (int i = threadIdx.x; i < 64 * 64 * BPP; i += 256) {
+        const int cc = i / (64 * BPP), rb = i % (64 * BPP);
+        const int rr = rb / BPP, ch = rb % BPP;
+        const int c = c0 + cc, r = r0 + rr;
+        if (c < cols && r < rows) dst[(long long)c * dst_pitch + (long long)r * BPP + ch] = tile[rr][cc * BPP + ch];
+    }
+}
+
+hipError_t launch_transpose_u8(const uint8_t* src, long long src_pitch, int rows, int cols, int bpp,
+                               uint8_t* dst, long long dst_pitch, hipStream_t s)
+{
+    dim3 grid((cols + 63) / 64, (rows + 63) / 64);
+    switch (bpp) {
+    case 1: hipLaunchKernelGGL(dcte_transpose_u8<1>, grid, dim3(256), 0, s, src, src_pitch, rows, cols, dst, dst_pitch); break;
+    case 3: hipLaunchKernelGGL(dcte_transpose_u8<3>, grid, dim3(256), 0, s, src, src_pitch, rows, cols, dst, dst_pitch); break;
+    case 4: hipLaunchKernelGGL(dcte_transpose_u8<4>, grid, dim3(256), 0, s, src, src_pitch, rows, cols, dst, dst_pitch); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace dcte

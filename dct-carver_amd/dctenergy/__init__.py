@@ -188,10 +188,11 @@ class Context:
         if px.strides[-1] != 1 or (px.ndim == 3 and px.strides[1] != bpp):
             px = np.ascontiguousarray(px)
         rowstride = px.strides[0]
+        shape = (w, h) if transposed else (h, w)
         if out is None:
-            out = np.empty((h, w), np.float32)
-        elif out.shape != (h, w) or out.dtype != np.float32 or not out.flags.c_contiguous:
-            raise ValueError("out must be a C-contiguous HxW float32 array")
+            out = np.empty(shape, np.float32)
+        elif out.shape != shape or out.dtype != np.float32 or not out.flags.c_contiguous:
+            raise ValueError(f"out must be a C-contiguous {shape} float32 array")
         self._check(lib().dcte_energy_map(self._h, px.ctypes.data, w, h, bpp, rowstride, n,
                                           edges, textures, semantics, int(bool(transposed)),
                                           out.ctypes.data))

@@ -27,7 +27,8 @@ static dcte_ctx *plugin_ctx(void)
 }
 
 int dcte_plugin_build(dcte_map_cache *c, const uint8_t *px, int w, int h, int bpp,
-                      size_t rowstride, int blocksize, float edges, float textures)
+                      size_t rowstride, int blocksize, float edges, float textures,
+                      int with_transposed)
 {
     if (!c) return DCTE_EINVAL;
     memset(c, 0, sizeof(*c));
@@ -38,10 +39,18 @@ int dcte_plugin_build(dcte_map_cache *c, const uint8_t *px, int w, int h, int bp
     if (!c->map) return c->status = DCTE_ENOMEM;
     c->status = dcte_energy_map(ctx, px, w, h, bpp, rowstride, blocksize, edges, textures,
                                 DCTE_LQR, 0, c->map);
+    if (c->status == DCTE_OK && with_transposed) {
+        c->map_t = (float *)malloc(sizeof(float) * (size_t)w * (size_t)h);
+        c->status = c->map_t ? dcte_energy_map(ctx, px, w, h, bpp, rowstride, blocksize, edges,
+                                               textures, DCTE_LQR, 1, c->map_t)
+                             : DCTE_ENOMEM;
+    }
     if (c->status != DCTE_OK) {
+        int st = c->status;
         free(c->map);
-        c->map = NULL;
-        return c->status;
+        free(c->map_t);
+        memset(c, 0, sizeof(*c));
+        return c->status = st;
     }
     c->w = w;
     c->h = h;
@@ -52,15 +61,22 @@ int dcte_plugin_build(dcte_map_cache *c, const uint8_t *px, int w, int h, int bp
 int dcte_plugin_lookup(const dcte_map_cache *c, int x, int y, int w, int h, int orientation,
                        float *out)
 {
-    if (!c || !c->valid || orientation != 0 || w != c->w || h != c->h) return 0;
-    if (x < 0 || y < 0 || x >= w || y >= h) return 0;
-    *out = c->map[(size_t)y * (size_t)w + (size_t)x];
-    return 1;
+    if (!c || !c->valid || x < 0 || y < 0 || x >= w || y >= h) return 0;
+    if (orientation == 0 && w == c->w && h == c->h) {
+        *out = c->map[(size_t)y * (size_t)w + (size_t)x];
+        return 1;
+    }
+    if (orientation == 1 && c->map_t && w == c->h && h == c->w) {
+        *out = c->map_t[(size_t)y * (size_t)w + (size_t)x];
+        return 1;
+    }
+    return 0;
 }
 
 void dcte_plugin_release(dcte_map_cache *c)
 {
     if (!c) return;
     free(c->map);
+    free(c->map_t);
     memset(c, 0, sizeof(*c));
 }

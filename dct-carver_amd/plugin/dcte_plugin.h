@@ -22,20 +22,26 @@ extern "C" {
 #endif
 
 typedef struct {
-    float *map;      /* w*h energies, row-major, owned */
-    int w, h;
+    float *map;      /* w*h energies of the frame (orientation 0), owned */
+    float *map_t;    /* h*w energies of the transposed frame (orientation 1), or NULL */
+    int w, h;        /* frame size */
     int valid;
     int status;      /* DCTE_* code of the last build */
 } dcte_map_cache;
 
-/* Build the map for the frame handed to lqr_carver_new (src/render.c:312).
- * Returns DCTE_OK, or an error code after which the cache stays invalid
- * and every lookup misses (the plug-in then runs its original code). */
+/* Build the map(s) for the frame handed to lqr_carver_new (src/render.c:312):
+ * orientation 0 always, and the transposed frame's map too when
+ * `with_transposed` (the plug-in passes vals->vertically, src/main.h:21:
+ * liblqr transposes the carver for vertical resizes).  Returns DCTE_OK, or
+ * an error code after which every lookup misses (the plug-in then runs its
+ * original code). */
 int dcte_plugin_build(dcte_map_cache *c, const uint8_t *px, int w, int h, int bpp,
-                      size_t rowstride, int blocksize, float edges, float textures);
+                      size_t rowstride, int blocksize, float edges, float textures,
+                      int with_transposed);
 
-/* 1 and *out = energy when (x, y) of a w x h carver in orientation 0 is
- * served from the map; 0 otherwise. */
+/* 1 and *out = energy when (x, y) of a w x h carver in `orientation` is
+ * served from a map (orientation 0: the frame's size; 1: the transposed
+ * frame's size, if that map was built); 0 otherwise. */
 int dcte_plugin_lookup(const dcte_map_cache *c, int x, int y, int w, int h,
                        int orientation, float *out);
 

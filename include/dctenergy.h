@@ -97,7 +97,9 @@ int dcte_set_option(dcte_ctx *ctx, int option, double value);
  *   n         blocksize N (2, 4, 8, 16)
  *   edges, textures   weights (PlugInVals, src/main.h:12-22)
  *   semantics DCTE_LQR or DCTE_PREVIEW
- *   transposed 0 (1 = map of the transposed frame; not in this build)
+ *   transposed 1 = the map of the transposed frame (what the callback returns
+ *             once liblqr has transposed the carver for a vertical resize);
+ *             out then holds w rows of h floats
  *   out       caller-owned w*h floats, row-major
  * With several devices the frame is split into row bands; each device
  * receives its band plus the N/2-row halo straight from `px`. */

@@ -64,22 +64,27 @@ static float original_dct_pixel_energy(int x, int y, int w, int h, LqrReadingWin
     return orc_window_energy(n, d, p->edges, p->textures);
 }
 
+static int g_orientation; /* lqr_carver_get_orientation of the fake carver */
+
 /* the PATCHED callback */
 static float dct_pixel_energy(int x, int y, int w, int h, LqrReadingWindow *rw, void *extra)
 {
     EnergyParameters *p = (EnergyParameters *)extra;
     float v;
-    if (dcte_plugin_lookup(&p->gpu, x, y, w, h, 0, &v)) return v;
+    if (dcte_plugin_lookup(&p->gpu, x, y, w, h, g_orientation, &v)) return v;
     return original_dct_pixel_energy(x, y, w, h, rw, extra);
 }
 
 /* Carver built on px (w x h, bpp), energy function registered with radius
  * n/2; then `removed` columns are dropped from the right (as if seams had
  * been carved) and the energy is rebuilt on the narrower carver.  out holds
- * the (w - removed) x h energies of that last build. */
+ * the (w - removed) x h energies of that last build.  transposed: the carver
+ * is transposed first (vertical resize: liblqr evaluates the energy on the
+ * transposed raw map, orientation 1); out is then h x (w - removed)... of the
+ * transposed frame: (w - removed) rows of h. */
 int fake_build_emap(const uint8_t *px, int w, int h, int bpp, int n, float edges, float textures,
-                    int use_gpu, int removed, float *out, long long *fallback_calls,
-                    int *gpu_status)
+                    int use_gpu, int removed, int transposed, float *out,
+                    long long *fallback_calls, int *gpu_status)
 {
     double *luma = (double *)malloc(sizeof(double) * (size_t)w * h);
     if (!luma) return -3;
@@ -90,26 +95,37 @@ int fake_build_emap(const uint8_t *px, int w, int h, int bpp, int n, float edges
                 : 0.2126 * ((double)q[0] / 255) + 0.7152 * ((double)q[1] / 255) + 0.0722 * ((double)q[2] / 255);
         }
     EnergyParameters p = {edges, textures, n, {0}};
-    *gpu_status = use_gpu ? dcte_plugin_build(&p.gpu, px, w, h, bpp, (size_t)w * bpp, n, edges, textures)
+    *gpu_status = use_gpu ? dcte_plugin_build(&p.gpu, px, w, h, bpp, (size_t)w * bpp, n, edges,
+                                              textures, transposed)
                           : DCTE_ENODEV;
-    int cw = w - removed;
-    double *cur = luma;
-    if (removed) {
-        cur = (double *)malloc(sizeof(double) * (size_t)cw * h);
+    /* the carver's current raw map: optionally transposed, then narrowed */
+    int fw = transposed ? h : w, fh = transposed ? w : h;
+    double *fr = luma;
+    if (transposed) {
+        fr = (double *)malloc(sizeof(double) * (size_t)w * h);
         for (int y = 0; y < h; y++)
-            for (int x = 0; x < cw; x++) cur[(size_t)y * cw + x] = luma[(size_t)y * w + x];
+            for (int x = 0; x < w; x++) fr[(size_t)x * h + y] = luma[(size_t)y * w + x];
+    }
+    int cw = fw - removed;
+    double *cur = fr;
+    if (removed) {
+        cur = (double *)malloc(sizeof(double) * (size_t)cw * fh);
+        for (int y = 0; y < fh; y++)
+            for (int x = 0; x < cw; x++) cur[(size_t)y * cw + x] = fr[(size_t)y * fw + x];
     }
     g_fallback_calls = 0;
-    LqrReadingWindow rw = {cur, cw, h, 0, 0, n / 2};
-    for (int y = 0; y < h; y++)
+    g_orientation = transposed;
+    LqrReadingWindow rw = {cur, cw, fh, 0, 0, n / 2};
+    for (int y = 0; y < fh; y++)
         for (int x = 0; x < cw; x++) {
             rw.x = x;
             rw.y = y;
-            out[(size_t)y * cw + x] = dct_pixel_energy(x, y, cw, h, &rw, &p);
+            out[(size_t)y * cw + x] = dct_pixel_energy(x, y, cw, fh, &rw, &p);
         }
     *fallback_calls = g_fallback_calls;
     dcte_plugin_release(&p.gpu);
-    if (cur != luma) free(cur);
+    if (cur != fr) free(cur);
+    if (fr != luma) free(fr);
     free(luma);
     return 0;
 }

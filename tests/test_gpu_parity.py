@@ -94,8 +94,8 @@ def test_bad_arguments(ctx):
         ctx.energy_map(np.zeros((16, 16, 2), np.uint8), 8)
     assert ei.value.code == dctenergy.DCTE_EINVAL
     with pytest.raises(dctenergy.DcteError) as ei:
-        ctx.energy_map(img, 8, transposed=True)
-    assert ei.value.code == dctenergy.DCTE_ENOTSUP
+        ctx.energy_map(img, 8, semantics=7)
+    assert ei.value.code == dctenergy.DCTE_EINVAL
 
 
 def _torch():
@@ -278,3 +278,16 @@ def test_preview_rejects_two_channels(ctx):
     with pytest.raises(dctenergy.DcteError) as ei:
         ctx.energy_map(np.zeros((8, 8, 2), np.uint8), 8, semantics=dctenergy.DCTE_PREVIEW)
     assert ei.value.code == dctenergy.DCTE_EINVAL
+
+
+@pytest.mark.parametrize("n", [2, 4, 8, 16])
+def test_transposed_map(ctx, n):
+    """transposed=1 is the map of the transposed frame (vertical carving)."""
+    for name in ("natural_rgb_73x59.npy", "natural_grey_200x120.npy", "tiny_rgb_5x1.npy"):
+        img = load_input(name)
+        tr = np.ascontiguousarray(np.swapaxes(img, 0, 1))
+        h, w = img.shape[:2]
+        out = np.empty((w, h), np.float32)
+        got = ctx.energy_map(img, n, 0.15, 0.85, transposed=True, out=out)
+        assert np.array_equal(got, ctx.energy_map(tr, n, 0.15, 0.85)), name
+        _assert_tol(got, O.energy_map(tr, n, 0.15, 0.85), name)
