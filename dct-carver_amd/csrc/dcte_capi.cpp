@@ -71,6 +71,17 @@ int hip_fail(dcte_ctx* ctx, hipError_t e, const char* where)
     return e == hipErrorOutOfMemory ? DCTE_ENOMEM : DCTE_EHIP;
 }
 
+// argument errors carry the failed check in dcte_last_error
+int bad_arg(dcte_ctx* ctx, const char* what)
+{
+    if (ctx) ctx->last_error = std::string("invalid argument: ") + what;
+    return DCTE_EINVAL;
+}
+#define DCTE_ARG(ctx, cond)                                 \
+    do {                                                    \
+        if (!(cond)) return bad_arg((ctx), #cond);          \
+    } while (0)
+
 #define DCTE_HIP(ctx, expr)                                              \
     do {                                                                 \
         hipError_t e_ = (expr);                                          \
@@ -140,13 +151,13 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
                int bpp, int in_row0, int in_rows, int y0, int y1, int n, float edges,
                float textures, int sem, float* d_out, long long out_stride, hipStream_t s)
 {
-    if (!valid_n(n) || !valid_sem_bpp(sem, bpp) || w <= 0 || h <= 0) return DCTE_EINVAL;
-    if (y0 < 0 || y1 > h || y0 > y1 || !d_px || !d_out || out_stride < w) return DCTE_EINVAL;
-    if (rowstride < (long long)w * bpp) return DCTE_EINVAL;
+    DCTE_ARG(ctx, valid_n(n) && valid_sem_bpp(sem, bpp) && w > 0 && h > 0);
+    DCTE_ARG(ctx, y0 >= 0 && y1 <= h && y0 <= y1 && d_px && d_out && out_stride >= w);
+    DCTE_ARG(ctx, rowstride >= (long long)w * bpp);
     if (y1 == y0) return DCTE_OK;
     int lo, hi;
     needed_rows(n, sem, h, y0, y1, lo, hi);
-    if (lo < in_row0 || hi >= in_row0 + in_rows) return DCTE_EINVAL;
+    DCTE_ARG(ctx, lo >= in_row0 && hi < in_row0 + in_rows);
     // one buffer resource addresses the readable rows: < 4 GiB
     long long span = (long long)(in_rows - 1) * rowstride + (long long)w * bpp + 3;
     if (span >= (1LL << 32)) return DCTE_ERANGE;
@@ -392,9 +403,9 @@ int dcte_energy_map_device(dcte_ctx* ctx, int device, const void* d_px, long lon
 int dcte_energy_map(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride,
                     int n, float edges, float textures, int semantics, int transposed, float* out)
 {
-    if (!ctx || !px || !out) return DCTE_EINVAL;
-    if (!valid_n(n) || !valid_sem_bpp(semantics, bpp) || w <= 0 || h <= 0) return DCTE_EINVAL;
-    if (rowstride < (size_t)w * bpp) return DCTE_EINVAL;
+    if (!ctx) return DCTE_EINVAL;
+    DCTE_ARG(ctx, px && out && valid_n(n) && valid_sem_bpp(semantics, bpp) && w > 0 && h > 0);
+    DCTE_ARG(ctx, rowstride >= (size_t)w * bpp);
     ctx->last_refined = 0;
     int G = 0;
     int rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, transposed, &G);
@@ -415,9 +426,9 @@ int dcte_energy_image_u8(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp
                          size_t rowstride, int n, float edges, float textures, int semantics,
                          int mode, int channels, uint8_t* out)
 {
-    if (!ctx || !px || !out) return DCTE_EINVAL;
-    if (!valid_n(n) || !valid_sem_bpp(semantics, bpp) || w <= 0 || h <= 0) return DCTE_EINVAL;
-    if (rowstride < (size_t)w * bpp || !valid_norm(mode, channels)) return DCTE_EINVAL;
+    if (!ctx) return DCTE_EINVAL;
+    DCTE_ARG(ctx, px && out && valid_n(n) && valid_sem_bpp(semantics, bpp) && w > 0 && h > 0);
+    DCTE_ARG(ctx, rowstride >= (size_t)w * bpp && valid_norm(mode, channels));
     ctx->last_refined = 0;
     int G = 0;
     int rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, 0, &G);

@@ -44,6 +44,11 @@ EXPORTS = ("dcte_abi_version", "dcte_device_count", "dcte_create", "dcte_destroy
 _lib = None
 
 
+def _rowstride(px):
+    """Bytes between rows; numpy leaves the stride of a 1-row array arbitrary."""
+    return px.strides[0] if px.shape[0] > 1 else px.shape[1] * (px.shape[2] if px.ndim == 3 else 1)
+
+
 class DcteError(RuntimeError):
     def __init__(self, code, detail=""):
         self.code = code
@@ -187,7 +192,7 @@ class Context:
             raise ValueError("px must be HxW or HxWxC")
         if px.strides[-1] != 1 or (px.ndim == 3 and px.strides[1] != bpp):
             px = np.ascontiguousarray(px)
-        rowstride = px.strides[0]
+        rowstride = _rowstride(px)
         shape = (w, h) if transposed else (h, w)
         if out is None:
             out = np.empty(shape, np.float32)
@@ -212,7 +217,7 @@ class Context:
         h, w = px.shape[:2]
         bpp = 1 if px.ndim == 2 else px.shape[2]
         out = np.empty((h, w) + ((channels,) if channels > 1 else ()), np.uint8)
-        self._check(lib().dcte_energy_image_u8(self._h, px.ctypes.data, w, h, bpp, px.strides[0],
+        self._check(lib().dcte_energy_image_u8(self._h, px.ctypes.data, w, h, bpp, _rowstride(px),
                                                n, edges, textures, semantics, mode, channels,
                                                out.ctypes.data))
         return out
