@@ -45,6 +45,9 @@ struct Device {
     size_t u8_cap = 0;
     uint8_t* d_tr = nullptr;       // transposed band (transposed maps)
     size_t tr_cap = 0;
+    hipStream_t up = nullptr;      // host path: H2D copies
+    hipStream_t down = nullptr;    // host path: D2H copies
+    std::vector<hipEvent_t> ev;    // host path: chunk hand-offs
 };
 
 }  // namespace
@@ -58,6 +61,7 @@ struct dcte_ctx {
     std::vector<Device> devs;
     double tie_tau = kDefaultTieTau;
     bool profile = false;
+    double pin_mib = 64.0;          // DCTE_OPT_PIN_HOST
     std::vector<ProfEvent> prof;
     long long last_refined = 0;
     std::string last_error;
@@ -116,9 +120,9 @@ bool valid_sem_bpp(int sem, int bpp)
 int ensure_fix(dcte_ctx* ctx, Device& d, hipStream_t s, size_t npix, FixScratch** out)
 {
     FixScratch& f = d.fix[s];
-    if (!f.d_count) {
-        DCTE_HIP(ctx, hipMalloc(&f.d_count, sizeof(unsigned)));
-        DCTE_HIP(ctx, hipMemset(f.d_count, 0, sizeof(unsigned)));
+    if (!f.d_count) {   // [0] flagged by the current launch, [1] refined since reset
+        DCTE_HIP(ctx, hipMalloc(&f.d_count, 2 * sizeof(unsigned)));
+        DCTE_HIP(ctx, hipMemset(f.d_count, 0, 2 * sizeof(unsigned)));
     }
     if (f.cap < npix) {
         if (f.d_list) DCTE_HIP(ctx, hipFree(f.d_list));
@@ -147,6 +151,41 @@ void small_twiddles(int n, double ct[4])
     }
 }
 
+// kernel weights divide by this: hat units of dcte_math.h (C * N for N = 8, 16;
+// C for the unnormalised N = 2, 4) times the luma unit (1/1275000 for liblqr,
+// 1 for the preview's u8 luma)
+double weight_scale(int n, int sem)
+{
+    return (sem == DCTE_LQR ? dcte::kLumaScale : 1.0) * (n >= 8 ? (double)n : 1.0);
+}
+
+dcte::FixParams fix_params(const uint8_t* px, long long rowstride, int w, int h, int in_row0,
+                           int bpp, int n, int y0, int sem, float* out, long long out_stride,
+                           float edges, float textures, const FixScratch* f)
+{
+    dcte::FixParams q{};
+    q.px = px;
+    q.rowstride = rowstride;
+    q.w = w;
+    q.h = h;
+    q.in_row0 = in_row0;
+    q.bpp = bpp;
+    q.n = n;
+    q.y0 = y0;
+    q.sem = sem;
+    q.out = out;
+    q.out_stride = out_stride;
+    q.edges = edges;
+    q.textures = textures;
+    small_twiddles(n, q.ct);
+    q.fix_count = f->d_count;
+    q.fix_list = f->d_list;
+    q.fix_cap = (unsigned)f->cap;
+    q.fix_total = f->d_count + 1;
+    q.pts = nullptr;
+    return q;
+}
+
 int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, int w, int h,
                int bpp, int in_row0, int in_rows, int y0, int y1, int n, float edges,
                float textures, int sem, float* d_out, long long out_stride, hipStream_t s)
@@ -171,8 +210,7 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     int rc = ensure_fix(ctx, d, s, npix, &f);
     if (rc) return rc;
 
-    // hat units (dcte_math.h): C * (N or 1); luma units: 1/1275000 (liblqr) or u8
-    const double scale = (sem == DCTE_LQR ? dcte::kLumaScale : 1.0) * (n >= 8 ? (double)n : 1.0);
+    const double scale = weight_scale(n, sem);
     dcte::MapParams p{};
     p.px = static_cast<const uint8_t*>(d_px);
     p.rowstride = rowstride;
@@ -194,24 +232,8 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     p.fix_list = f->d_list;
     p.fix_cap = (unsigned)f->cap;
 
-    dcte::FixParams q{};
-    q.px = p.px;
-    q.rowstride = rowstride;
-    q.w = w;
-    q.h = h;
-    q.in_row0 = in_row0;
-    q.bpp = bpp;
-    q.n = n;
-    q.y0 = y0;
-    q.sem = sem;
-    q.out = d_out;
-    q.out_stride = out_stride;
-    q.edges = edges;
-    q.textures = textures;
-    small_twiddles(n, q.ct);
-    q.fix_count = f->d_count;
-    q.fix_list = f->d_list;
-    q.fix_cap = (unsigned)f->cap;
+    dcte::FixParams q = fix_params(p.px, rowstride, w, h, in_row0, bpp, n, y0, sem, d_out,
+                                   out_stride, edges, textures, f);
 
     DCTE_HIP(ctx, hipMemsetAsync(f->d_count, 0, sizeof(unsigned), s));
     if (ctx->profile) {
@@ -257,16 +279,62 @@ bool valid_norm(int mode, int channels)
     return (mode == DCTE_NORM_LQR || mode == DCTE_NORM_PREVIEW) && channels >= 1 && channels <= 4;
 }
 
+// Page-locks a caller buffer for the duration of a host call (RAII).  A
+// buffer that is already pinned, or that the runtime refuses, stays as it is:
+// pinning only lets the chunk copies overlap, it never changes results.
+struct HostPin {
+    void* base = nullptr;
+    HostPin(const dcte_ctx* ctx, const void* p, size_t bytes)
+    {
+        if (ctx->pin_mib <= 0 || (double)bytes < ctx->pin_mib * 1048576.0) return;
+        const uintptr_t pg = 4096;
+        uintptr_t a = reinterpret_cast<uintptr_t>(p) & ~(pg - 1);
+        uintptr_t b = (reinterpret_cast<uintptr_t>(p) + bytes + pg - 1) & ~(pg - 1);
+        void* v = reinterpret_cast<void*>(a);
+        if (hipHostRegister(v, b - a, hipHostRegisterDefault) == hipSuccess) base = v;
+        else (void)hipGetLastError();
+    }
+    ~HostPin()
+    {
+        if (base) (void)hipHostUnregister(base);
+    }
+    HostPin(const HostPin&) = delete;
+    HostPin& operator=(const HostPin&) = delete;
+};
+
+constexpr int kChunkRows = 2048;   // host path: output rows per pipeline chunk
+constexpr int kMaxChunks = 16;
+
+int ensure_pipe(dcte_ctx* ctx, Device& d, size_t nev)
+{
+    DCTE_HIP(ctx, hipSetDevice(d.id));
+    if (!d.up) DCTE_HIP(ctx, hipStreamCreateWithFlags(&d.up, hipStreamNonBlocking));
+    if (!d.down) DCTE_HIP(ctx, hipStreamCreateWithFlags(&d.down, hipStreamNonBlocking));
+    while (d.ev.size() < nev) {
+        hipEvent_t e;
+        DCTE_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        d.ev.push_back(e);
+    }
+    return DCTE_OK;
+}
+
 // host frame -> device band maps (rows split over the context's devices),
 // left on the devices in d.d_out; returns the number of devices used.
+// Each band runs as a pipeline of row chunks on three streams -- H2D of the
+// rows chunk c needs (up), its map (d.stream), D2H of its output rows into
+// host_out when given (down) -- so the PCIe copies of neighbouring chunks
+// overlap each other and the kernels.
 // transposed: the map of the transposed frame (w x h -> h x w); device k
 // takes a strip of source COLUMNS (= transposed rows) plus halo, transposes
-// it in HBM and maps it.
+// it in HBM and maps it (one chunk).
 int map_bands(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride, int n,
-              float edges, float textures, int sem, int transposed, int* used)
+              float edges, float textures, int sem, int transposed, float* host_out, int* used)
 {
     const int W = transposed ? h : w, H = transposed ? w : h;   // mapped frame
     const int G = (int)ctx->devs.size() < H ? (int)ctx->devs.size() : H;
+    *used = G;                         // even on error: the caller drains these streams
+    int hl, hr;
+    halo(n, sem, hl, hr);
     for (int k = 0; k < G; k++) {
         Device& d = ctx->devs[k];
         int y0 = (int)((long long)H * k / G), y1 = (int)((long long)H * (k + 1) / G);
@@ -281,11 +349,11 @@ int map_bands(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t ro
         if (rc) return rc;
         rc = ensure_buf(ctx, (void**)&d.d_out, &d.out_cap, out_bytes);
         if (rc) return rc;
-        const uint8_t* band = d.d_in;
-        if (!transposed) {
-            DCTE_HIP(ctx, hipMemcpy2DAsync(d.d_in, pitch, px + (size_t)lo * rowstride, rowstride,
-                                           pitch, hi - lo + 1, hipMemcpyHostToDevice, d.stream));
-        } else {
+        FixScratch* f = nullptr;
+        rc = ensure_fix(ctx, d, d.stream, (size_t)W * (size_t)(y1 - y0), &f);
+        if (rc) return rc;
+        DCTE_HIP(ctx, hipMemsetAsync(f->d_count + 1, 0, sizeof(unsigned), d.stream));
+        if (transposed) {
             // source columns [lo, hi] of all h rows -> (h x cols) strip -> transpose
             const size_t sw = (size_t)(hi - lo + 1) * bpp;
             DCTE_HIP(ctx, hipMemcpy2DAsync(d.d_in, sw, px + (size_t)lo * bpp, rowstride, sw, h,
@@ -294,26 +362,74 @@ int map_bands(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t ro
             if (rc) return rc;
             DCTE_HIP(ctx, dcte::launch_transpose_u8(d.d_in, (long long)sw, h, hi - lo + 1, bpp,
                                                     d.d_tr, (long long)pitch, d.stream));
-            band = d.d_tr;
+            rc = run_device(ctx, d, d.d_tr, (long long)pitch, W, H, bpp, lo, hi - lo + 1, y0, y1,
+                            n, edges, textures, sem, d.d_out, W, d.stream);
+            if (rc) return rc;
+            if (host_out)
+                DCTE_HIP(ctx, hipMemcpyAsync(host_out + (size_t)y0 * W, d.d_out, out_bytes,
+                                             hipMemcpyDeviceToHost, d.stream));
+            continue;
         }
-        rc = run_device(ctx, d, band, (long long)pitch, W, H, bpp, lo, hi - lo + 1, y0, y1, n,
-                        edges, textures, sem, d.d_out, W, d.stream);
+        int nch = (y1 - y0 + kChunkRows - 1) / kChunkRows;
+        nch = nch < 1 ? 1 : (nch > kMaxChunks ? kMaxChunks : nch);
+        rc = ensure_pipe(ctx, d, 2 * (size_t)nch);
         if (rc) return rc;
+        int loaded = lo - 1;                                    // last uploaded row
+        for (int c = 0; c < nch; c++) {
+            const int a = y0 + (int)((long long)(y1 - y0) * c / nch);
+            const int b = y0 + (int)((long long)(y1 - y0) * (c + 1) / nch);
+            if (a == b) continue;
+            const int need = b - 1 + hr < H - 1 ? b - 1 + hr : H - 1;
+            hipEvent_t ev_up = d.ev[2 * c], ev_map = d.ev[2 * c + 1];
+            if (need > loaded) {
+                DCTE_HIP(ctx, hipMemcpy2DAsync(d.d_in + (size_t)(loaded + 1 - lo) * pitch, pitch,
+                                               px + (size_t)(loaded + 1) * rowstride, rowstride,
+                                               pitch, need - loaded, hipMemcpyHostToDevice, d.up));
+                loaded = need;
+            }
+            DCTE_HIP(ctx, hipEventRecord(ev_up, d.up));
+            DCTE_HIP(ctx, hipStreamWaitEvent(d.stream, ev_up, 0));
+            rc = run_device(ctx, d, d.d_in, (long long)pitch, W, H, bpp, lo, loaded - lo + 1, a, b,
+                            n, edges, textures, sem, d.d_out + (size_t)(a - y0) * W, W, d.stream);
+            if (rc) return rc;
+            if (host_out) {
+                DCTE_HIP(ctx, hipEventRecord(ev_map, d.stream));
+                DCTE_HIP(ctx, hipStreamWaitEvent(d.down, ev_map, 0));
+                DCTE_HIP(ctx, hipMemcpyAsync(host_out + (size_t)a * W, d.d_out + (size_t)(a - y0) * W,
+                                             sizeof(float) * (size_t)W * (size_t)(b - a),
+                                             hipMemcpyDeviceToHost, d.down));
+            }
+        }
     }
-    *used = G;
     return DCTE_OK;
 }
+
+// error path: wait for every stream of the first G devices, keep last_error
+void drain(dcte_ctx* ctx, int G)
+{
+    for (int k = 0; k < G; k++) {
+        Device& d = ctx->devs[k];
+        if (hipSetDevice(d.id) != hipSuccess) continue;
+        if (d.up) (void)hipStreamSynchronize(d.up);
+        if (d.stream) (void)hipStreamSynchronize(d.stream);
+        if (d.down) (void)hipStreamSynchronize(d.down);
+    }
+}
+
+int normalize_bands(dcte_ctx* ctx, int w, int h, int mode, int channels, uint8_t* out, int G);
 
 int sync_bands(dcte_ctx* ctx, int G)
 {
     for (int k = 0; k < G; k++) {
         Device& d = ctx->devs[k];
         DCTE_HIP(ctx, hipSetDevice(d.id));
+        if (d.up) DCTE_HIP(ctx, hipStreamSynchronize(d.up));
         DCTE_HIP(ctx, hipStreamSynchronize(d.stream));
+        if (d.down) DCTE_HIP(ctx, hipStreamSynchronize(d.down));
         auto it = d.fix.find(d.stream);
         if (it != d.fix.end()) {
             unsigned cnt = 0;
-            DCTE_HIP(ctx, hipMemcpy(&cnt, it->second.d_count, sizeof(unsigned), hipMemcpyDeviceToHost));
+            DCTE_HIP(ctx, hipMemcpy(&cnt, it->second.d_count + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
             ctx->last_refined += cnt;
         }
     }
@@ -368,6 +484,11 @@ void dcte_destroy(dcte_ctx* ctx)
         if (d.d_keys) (void)hipFree(d.d_keys);
         if (d.d_u8) (void)hipFree(d.d_u8);
         if (d.d_tr) (void)hipFree(d.d_tr);
+        if (d.up) (void)hipStreamSynchronize(d.up);
+        if (d.down) (void)hipStreamSynchronize(d.down);
+        for (hipEvent_t e : d.ev) (void)hipEventDestroy(e);
+        if (d.up) (void)hipStreamDestroy(d.up);
+        if (d.down) (void)hipStreamDestroy(d.down);
         if (d.stream) (void)hipStreamDestroy(d.stream);
     }
     delete ctx;
@@ -386,6 +507,10 @@ int dcte_set_option(dcte_ctx* ctx, int option, double value)
     case DCTE_OPT_PROFILE:
         ctx->profile = value != 0;
         return DCTE_OK;
+    case DCTE_OPT_PIN_HOST:
+        if (!(value >= 0)) return DCTE_EINVAL;
+        ctx->pin_mib = value;
+        return DCTE_OK;
     default: return DCTE_EINVAL;
     }
 }
@@ -400,6 +525,143 @@ int dcte_energy_map_device(dcte_ctx* ctx, int device, const void* d_px, long lon
                       y1, n, edges, textures, semantics, d_out, out_stride, (hipStream_t)stream);
 }
 
+int dcte_seam_carve_device(dcte_ctx* ctx, int device, const void* d_px, long long rowstride, int w,
+                           int h, int bpp, const int* d_seam, const float* d_map,
+                           long long map_stride, void* d_px_out, long long out_rowstride,
+                           float* d_map_out, long long map_out_stride, int n, float edges,
+                           float textures, int semantics, void* stream)
+{
+    if (!ctx) return DCTE_EINVAL;
+    DCTE_ARG(ctx, device >= 0 && device < (int)ctx->devs.size());
+    DCTE_ARG(ctx, valid_n(n) && valid_sem_bpp(semantics, bpp) && w >= 2 && h >= 1);
+    DCTE_ARG(ctx, d_px && d_seam && d_map && d_px_out && d_map_out);
+    DCTE_ARG(ctx, rowstride >= (long long)w * bpp && out_rowstride >= (long long)(w - 1) * bpp);
+    DCTE_ARG(ctx, map_stride >= w && map_out_stride >= w - 1);
+    Device& d = ctx->devs[device];
+    hipStream_t s = (hipStream_t)stream;
+    DCTE_HIP(ctx, hipSetDevice(d.id));
+    FixScratch* f = nullptr;
+    const size_t npix = (size_t)(w - 1) * (size_t)h;
+    if (npix >= (1ULL << 32)) return DCTE_ERANGE;
+    int rc = ensure_fix(ctx, d, s, npix, &f);
+    if (rc) return rc;
+    const double scale = weight_scale(n, semantics);
+    dcte::SeamParams p{};
+    p.px = static_cast<const uint8_t*>(d_px);
+    p.rowstride = rowstride;
+    p.w = w;
+    p.h = h;
+    p.bpp = bpp;
+    p.n = n;
+    p.sem = semantics;
+    p.seam = d_seam;
+    p.map = d_map;
+    p.map_stride = map_stride;
+    p.px_out = static_cast<uint8_t*>(d_px_out);
+    p.out_rowstride = out_rowstride;
+    p.map_out = d_map_out;
+    p.map_out_stride = map_out_stride;
+    p.we = (float)((double)edges / scale);
+    p.wt = (float)((double)textures / scale);
+    p.tie_tau = (float)ctx->tie_tau;
+    p.fix_count = f->d_count;
+    p.fix_list = f->d_list;
+    p.fix_cap = (unsigned)f->cap;
+    DCTE_HIP(ctx, hipMemsetAsync(f->d_count, 0, sizeof(unsigned), s));
+    DCTE_HIP(ctx, dcte::launch_seam_carve(p, s));
+    if ((p.we != p.wt && ctx->tie_tau > 0) || ctx->tie_tau >= 1.0) {
+        dcte::FixParams q = fix_params(p.px_out, out_rowstride, w - 1, h, 0, bpp, n, 0, semantics,
+                                       d_map_out, map_out_stride, edges, textures, f);
+        DCTE_HIP(ctx, dcte::launch_fix(q, s));
+    }
+    return DCTE_OK;
+}
+
+int dcte_energy_points_device(dcte_ctx* ctx, int device, const void* d_px, long long rowstride,
+                              int w, int h, int bpp, const int* d_xy, int count, int n,
+                              float edges, float textures, int semantics, float* d_out,
+                              void* stream)
+{
+    if (!ctx) return DCTE_EINVAL;
+    DCTE_ARG(ctx, device >= 0 && device < (int)ctx->devs.size());
+    DCTE_ARG(ctx, valid_n(n) && valid_sem_bpp(semantics, bpp) && w >= 1 && h >= 1 && count >= 0);
+    DCTE_ARG(ctx, rowstride >= (long long)w * bpp);
+    if (count == 0) return DCTE_OK;
+    DCTE_ARG(ctx, d_px && d_xy && d_out);
+    Device& d = ctx->devs[device];
+    hipStream_t s = (hipStream_t)stream;
+    DCTE_HIP(ctx, hipSetDevice(d.id));
+    FixScratch* f = nullptr;
+    int rc = ensure_fix(ctx, d, s, (size_t)count, &f);
+    if (rc) return rc;
+    const double scale = weight_scale(n, semantics);
+    dcte::SeamParams p{};
+    p.px = static_cast<const uint8_t*>(d_px);
+    p.rowstride = rowstride;
+    p.w = w;
+    p.h = h;
+    p.bpp = bpp;
+    p.n = n;
+    p.sem = semantics;
+    p.in_row0 = 0;
+    p.pts = d_xy;
+    p.count = count;
+    p.map_out = d_out;
+    p.we = (float)((double)edges / scale);
+    p.wt = (float)((double)textures / scale);
+    p.tie_tau = (float)ctx->tie_tau;
+    p.fix_count = f->d_count;
+    p.fix_list = f->d_list;
+    p.fix_cap = (unsigned)f->cap;
+    DCTE_HIP(ctx, hipMemsetAsync(f->d_count, 0, sizeof(unsigned), s));
+    DCTE_HIP(ctx, dcte::launch_points(p, s));
+    if ((p.we != p.wt && ctx->tie_tau > 0) || ctx->tie_tau >= 1.0) {
+        dcte::FixParams q = fix_params(p.px, rowstride, w, h, 0, bpp, n, 0, semantics, d_out, 0,
+                                       edges, textures, f);
+        q.pts = d_xy;
+        DCTE_HIP(ctx, dcte::launch_fix(q, s));
+    }
+    return DCTE_OK;
+}
+
+int dcte_energy_points(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride,
+                       const int* xy, int count, int n, float edges, float textures, int semantics,
+                       float* out)
+{
+    if (!ctx) return DCTE_EINVAL;
+    DCTE_ARG(ctx, valid_n(n) && valid_sem_bpp(semantics, bpp) && w >= 1 && h >= 1 && count >= 0);
+    DCTE_ARG(ctx, rowstride >= (size_t)w * bpp);
+    if (count == 0) return DCTE_OK;
+    DCTE_ARG(ctx, px && xy && out);
+    for (int k = 0; k < count; k++)
+        DCTE_ARG(ctx, xy[2 * k] >= 0 && xy[2 * k] < w && xy[2 * k + 1] >= 0 && xy[2 * k + 1] < h);
+    ctx->last_refined = 0;
+    Device& d = ctx->devs[0];
+    int rc = ensure_stream(ctx, d);
+    if (rc) return rc;
+    // frame rows packed, then the points (4-byte aligned)
+    const size_t frame = (size_t)w * bpp * (size_t)h, pts = sizeof(int) * 2 * (size_t)count;
+    const size_t pts_off = (frame + 3) & ~(size_t)3;
+    rc = ensure_buf(ctx, (void**)&d.d_in, &d.in_cap, pts_off + pts);
+    if (rc) return rc;
+    rc = ensure_buf(ctx, (void**)&d.d_out, &d.out_cap, sizeof(float) * (size_t)count);
+    if (rc) return rc;
+    DCTE_HIP(ctx, hipMemcpy2DAsync(d.d_in, (size_t)w * bpp, px, rowstride, (size_t)w * bpp, h,
+                                   hipMemcpyHostToDevice, d.stream));
+    int* d_xy = reinterpret_cast<int*>(d.d_in + pts_off);
+    DCTE_HIP(ctx, hipMemcpyAsync(d_xy, xy, pts, hipMemcpyHostToDevice, d.stream));
+    FixScratch* f = nullptr;
+    rc = ensure_fix(ctx, d, d.stream, (size_t)count, &f);
+    if (rc) return rc;
+    DCTE_HIP(ctx, hipMemsetAsync(f->d_count + 1, 0, sizeof(unsigned), d.stream));
+    rc = dcte_energy_points_device(ctx, 0, d.d_in, (long long)w * bpp, w, h, bpp, d_xy, count, n,
+                                   edges, textures, semantics, d.d_out, d.stream);
+    if (rc) return rc;
+    DCTE_HIP(ctx, hipMemcpyAsync(out, d.d_out, sizeof(float) * (size_t)count,
+                                 hipMemcpyDeviceToHost, d.stream));
+    return sync_bands(ctx, 1);
+}
+
 int dcte_energy_map(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride,
                     int n, float edges, float textures, int semantics, int transposed, float* out)
 {
@@ -407,17 +669,14 @@ int dcte_energy_map(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, siz
     DCTE_ARG(ctx, px && out && valid_n(n) && valid_sem_bpp(semantics, bpp) && w > 0 && h > 0);
     DCTE_ARG(ctx, rowstride >= (size_t)w * bpp);
     ctx->last_refined = 0;
+    HostPin pin_in(ctx, px, (size_t)(h - 1) * rowstride + (size_t)w * bpp);
+    HostPin pin_out(ctx, out, sizeof(float) * (size_t)w * (size_t)h);
     int G = 0;
-    int rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, transposed, &G);
-    if (rc) return rc;
-    const int W = transposed ? h : w, H = transposed ? w : h;
-    for (int k = 0; k < G; k++) {
-        Device& d = ctx->devs[k];
-        int y0 = (int)((long long)H * k / G), y1 = (int)((long long)H * (k + 1) / G);
-        DCTE_HIP(ctx, hipSetDevice(d.id));
-        DCTE_HIP(ctx, hipMemcpyAsync(out + (size_t)y0 * W, d.d_out,
-                                     sizeof(float) * (size_t)W * (size_t)(y1 - y0),
-                                     hipMemcpyDeviceToHost, d.stream));
+    int rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, transposed,
+                       out, &G);
+    if (rc) {
+        drain(ctx, G);              // nothing in flight may still use px / out
+        return rc;
     }
     return sync_bands(ctx, G);
 }
@@ -431,8 +690,26 @@ int dcte_energy_image_u8(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp
     DCTE_ARG(ctx, rowstride >= (size_t)w * bpp && valid_norm(mode, channels));
     ctx->last_refined = 0;
     int G = 0;
-    int rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, 0, &G);
-    if (rc) return rc;
+    HostPin pin_in(ctx, px, (size_t)(h - 1) * rowstride + (size_t)w * bpp);
+    HostPin pin_out(ctx, out, (size_t)w * (size_t)h * (size_t)channels);
+    int rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, 0, nullptr,
+                       &G);
+    if (rc == DCTE_OK) rc = normalize_bands(ctx, w, h, mode, channels, out, G);
+    if (rc) {
+        drain(ctx, G);              // nothing in flight may still use px / out
+        return rc;
+    }
+    return sync_bands(ctx, G);
+}
+
+}  // extern "C"
+
+namespace {
+
+// energy_image_u8, second half: global min/max over the band maps, then u8
+int normalize_bands(dcte_ctx* ctx, int w, int h, int mode, int channels, uint8_t* out, int G)
+{
+    int rc;
     // per-band min/max, reduced on the host (2 floats per device)
     float gmin = 0, gmax = 0;
     for (int k = 0; k < G; k++) {
@@ -459,8 +736,12 @@ int dcte_energy_image_u8(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp
         DCTE_HIP(ctx, hipMemcpyAsync(out + (size_t)y0 * w * channels, d.d_u8, npx * channels,
                                      hipMemcpyDeviceToHost, d.stream));
     }
-    return sync_bands(ctx, G);
+    return DCTE_OK;
 }
+
+}  // namespace
+
+extern "C" {
 
 int dcte_normalize_u8(dcte_ctx* ctx, const float* E, size_t n, int mode, int channels, uint8_t* out)
 {

@@ -42,11 +42,36 @@ struct FixParams {
     unsigned* fix_count;     // pixels flagged by the map kernel
     unsigned* fix_list;
     unsigned fix_cap;
+    unsigned* fix_total;     // += pixels refined (host-path diagnostic), or null
+    const int* pts;          // points mode: entry k is point k = (pts[2k], pts[2k+1]) -> out[k]
+};
+
+// Seam removal + energy update (dcte_seam.hip) and energies at points.
+struct SeamParams {
+    const uint8_t* px;       // source frame, w x h, row 0 .. h - 1 readable
+    long long rowstride;
+    int w, h, bpp, n, sem;
+    int in_row0;             // points: global row addressed by px
+    const int* seam;         // h column indices (carve)
+    const float* map;        // energies of the source frame (carve)
+    long long map_stride;
+    uint8_t* px_out;         // (w - 1) x h carved frame (carve)
+    long long out_rowstride;
+    float* map_out;          // carve: (w - 1) x h energies; points: count energies
+    long long map_out_stride;
+    const int* pts;          // points: (x, y) pairs
+    int count;
+    float we, wt, tie_tau;   // as MapParams
+    unsigned* fix_count;
+    unsigned* fix_list;
+    unsigned fix_cap;
 };
 
 // host-side launchers (dcte_kernels.hip)
 hipError_t launch_map(int n, int bpp, int sem, const MapParams& p, hipStream_t s);
 hipError_t launch_fix(const FixParams& p, hipStream_t s);
+hipError_t launch_seam_carve(const SeamParams& p, hipStream_t s);
+hipError_t launch_points(const SeamParams& p, hipStream_t s);
 
 // geometry the launcher uses (exported for tests / bench)
 int map_tile_w(int n);

@@ -282,10 +282,20 @@ __global__ __launch_bounds__(64 * kFixWaves) void dcte_fix(const FixParams p)
     double* d = win[wv];
     const unsigned cnt = min(*p.fix_count, p.fix_cap);
     constexpr int HL = Geo<N, SEM>::HL;
+    if (p.fix_total && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(p.fix_total, cnt);
     for (unsigned k = blockIdx.x * kFixWaves + wv; k < cnt; k += gridDim.x * kFixWaves) {
         const unsigned idx = p.fix_list[k];
-        const int y = p.y0 + (int)(idx / (unsigned)p.w);
-        const int x = (int)(idx % (unsigned)p.w);
+        int x, y;
+        long long o;                                   // output element
+        if (p.pts) {                                   // points mode
+            x = clampi(p.pts[2 * idx], 0, p.w - 1);
+            y = clampi(p.pts[2 * idx + 1], 0, p.h - 1);
+            o = idx;
+        } else {
+            y = p.y0 + (int)(idx / (unsigned)p.w);
+            x = (int)(idx % (unsigned)p.w);
+            o = (long long)(y - p.y0) * p.out_stride + x;
+        }
         for (int e = lane; e < N * N; e += 64) {
             // liblqr callback: data[dx][dy] (src/render.c:150);
             // preview: data[dy][dx] (src/render.c:49)
@@ -346,8 +356,7 @@ __global__ __launch_bounds__(64 * kFixWaves) void dcte_fix(const FixParams p)
         if (lane == 0) {
             const int k1 = bi / N, k2 = bi % N;
             const bool edge = (k1 == 0 && k2 == 1) || (k1 == 1 && k2 == 0);
-            p.out[(long long)(y - p.y0) * p.out_stride + x] =
-                edge ? (float)(best * (double)p.edges) : (float)(best * (double)p.textures);
+            p.out[o] = edge ? (float)(best * (double)p.edges) : (float)(best * (double)p.textures);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();

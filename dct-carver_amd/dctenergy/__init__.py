@@ -31,6 +31,7 @@ DCTE_LQR = 0
 DCTE_PREVIEW = 1
 DCTE_OPT_TIE_TAU = 1
 DCTE_OPT_PROFILE = 2
+DCTE_OPT_PIN_HOST = 3
 DCTE_NORM_LQR = 0
 DCTE_NORM_PREVIEW = 1
 
@@ -39,7 +40,8 @@ EXPORTS = ("dcte_abi_version", "dcte_device_count", "dcte_create", "dcte_destroy
            "dcte_ctx_devices", "dcte_set_option", "dcte_energy_map",
            "dcte_energy_map_device", "dcte_last_refined", "dcte_profile_read", "dcte_strerror",
            "dcte_last_error", "dcte_normalize_u8", "dcte_energy_image_u8", "dcte_minmax_device",
-           "dcte_normalize_u8_device")
+           "dcte_normalize_u8_device", "dcte_seam_carve_device", "dcte_energy_points",
+           "dcte_energy_points_device")
 
 _lib = None
 
@@ -72,6 +74,15 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise OSError(f"libdctenergy_hip.so not found at {LIB_PATH}; run __graft_entry__.build()")
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64
+    # (soname libamdhip64.so.7, loaded by the unversioned name).  Loaded after
+    # ours, it would come in as a second runtime and find no device; loaded
+    # first, our NEEDED libamdhip64.so.7 binds to it.  So torch goes first
+    # whenever it is installed.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp = ctypes.c_void_p
     L.dcte_abi_version.restype = ctypes.c_int
@@ -110,6 +121,14 @@ def lib():
     L.dcte_normalize_u8_device.restype = ctypes.c_int
     L.dcte_normalize_u8_device.argtypes = [vp, ctypes.c_int, vp, ctypes.c_longlong, vp,
                                            ctypes.c_int, ctypes.c_int, vp, vp]
+    i, f, ll = ctypes.c_int, ctypes.c_float, ctypes.c_longlong
+    L.dcte_seam_carve_device.restype = i
+    L.dcte_seam_carve_device.argtypes = [vp, i, vp, ll, i, i, i, vp, vp, ll, vp, ll, vp, ll, i, f, f,
+                                         i, vp]
+    L.dcte_energy_points.restype = i
+    L.dcte_energy_points.argtypes = [vp, vp, i, i, i, ctypes.c_size_t, vp, i, i, f, f, i, vp]
+    L.dcte_energy_points_device.restype = i
+    L.dcte_energy_points_device.argtypes = [vp, i, vp, ll, i, i, i, vp, i, i, f, f, i, vp, vp]
     L.dcte_strerror.restype = ctypes.c_char_p
     L.dcte_strerror.argtypes = [ctypes.c_int]
     L.dcte_last_error.restype = ctypes.c_char_p
@@ -266,7 +285,68 @@ class Context:
                                semantics)
         return out
 
+    # -- seam carving support
+    def energy_points(self, px, xy, n=8, edges=0.5, textures=0.5, semantics=DCTE_LQR):
+        """Energies of the listed pixels (K x 2 int array of (x, y)) of a host frame."""
+        px = np.asarray(px)
+        if px.dtype != np.uint8 or px.ndim not in (2, 3):
+            raise TypeError("px must be an HxW or HxWxC uint8 array")
+        px = np.ascontiguousarray(px)
+        h, w = px.shape[:2]
+        bpp = 1 if px.ndim == 2 else px.shape[2]
+        xy = np.ascontiguousarray(xy, dtype=np.int32).reshape(-1, 2)
+        out = np.empty(len(xy), np.float32)
+        self._check(lib().dcte_energy_points(self._h, px.ctypes.data, w, h, bpp, _rowstride(px),
+                                             xy.ctypes.data, len(xy), n, edges, textures,
+                                             semantics, out.ctypes.data))
+        return out
+
+    def energy_points_tensor(self, px, xy, out, n=8, edges=0.5, textures=0.5, stream=None,
+                             device=0, semantics=DCTE_LQR):
+        """Device version: px torch.uint8 frame, xy int32 [K, 2], out float32 [K]."""
+        import torch
+        if px.dtype != torch.uint8 or xy.dtype != torch.int32 or out.dtype != torch.float32:
+            raise TypeError("px uint8, xy int32, out float32")
+        if not (xy.is_contiguous() and out.is_contiguous()):
+            raise ValueError("xy and out must be contiguous")
+        h, w = px.shape[0], px.shape[1]
+        bpp = 1 if px.dim() == 2 else px.shape[2]
+        if stream is None:
+            stream = torch.cuda.current_stream(px.device).cuda_stream
+        self._check(lib().dcte_energy_points_device(
+            self._h, device, ctypes.c_void_p(px.data_ptr()), px.stride(0), w, h, bpp,
+            ctypes.c_void_p(xy.data_ptr()), xy.shape[0], n, edges, textures, semantics,
+            ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream)))
+        return out
+
+    def seam_carve_tensor(self, px, seam, emap, px_out, emap_out, n=8, edges=0.5, textures=0.5,
+                          stream=None, device=0, semantics=DCTE_LQR):
+        """Remove seam[y] from every row of the device frame px (H x W[xC]) ->
+        px_out (H x (W-1)[xC]); emap (map of px) -> emap_out (map of px_out)."""
+        import torch
+        if px.dtype != torch.uint8 or px_out.dtype != torch.uint8:
+            raise TypeError("frames must be uint8")
+        if seam.dtype != torch.int32 or not seam.is_contiguous():
+            raise TypeError("seam must be a contiguous int32 tensor")
+        if emap.dtype != torch.float32 or emap_out.dtype != torch.float32:
+            raise TypeError("maps must be float32")
+        h, w = px.shape[0], px.shape[1]
+        bpp = 1 if px.dim() == 2 else px.shape[2]
+        if seam.numel() != h or px_out.shape[0] != h or px_out.shape[1] != w - 1:
+            raise ValueError("seam needs h entries, px_out h x (w-1)")
+        if emap.shape[1] < w or emap_out.shape[1] < w - 1:
+            raise ValueError("map shapes")
+        if stream is None:
+            stream = torch.cuda.current_stream(px.device).cuda_stream
+        self._check(lib().dcte_seam_carve_device(
+            self._h, device, ctypes.c_void_p(px.data_ptr()), px.stride(0), w, h, bpp,
+            ctypes.c_void_p(seam.data_ptr()), ctypes.c_void_p(emap.data_ptr()), emap.stride(0),
+            ctypes.c_void_p(px_out.data_ptr()), px_out.stride(0),
+            ctypes.c_void_p(emap_out.data_ptr()), emap_out.stride(0), n, edges, textures,
+            semantics, ctypes.c_void_p(stream)))
+        return px_out, emap_out
+
 
 __all__ = ["Context", "DcteError", "lib", "device_count", "LIB_PATH", "EXPORTS",
-           "DCTE_LQR", "DCTE_PREVIEW", "DCTE_OPT_TIE_TAU", "DCTE_OPT_PROFILE",
+           "DCTE_LQR", "DCTE_PREVIEW", "DCTE_OPT_TIE_TAU", "DCTE_OPT_PROFILE", "DCTE_OPT_PIN_HOST",
            "DCTE_NORM_LQR", "DCTE_NORM_PREVIEW"]

@@ -72,6 +72,11 @@ extern "C" {
                               every pixel) */
 #define DCTE_OPT_PROFILE 2 /* 1 = bracket every map-kernel launch with HIP
                               events on its stream (dcte_profile_read) */
+#define DCTE_OPT_PIN_HOST 3 /* host entry points: page-lock the caller's frame
+                               and output for the duration of a call when they
+                               are at least this many MiB (default 64; 0 = never),
+                               so the chunked H2D / D2H copies overlap (pageable
+                               copies are staged serially by the runtime) */
 
 typedef struct dcte_ctx dcte_ctx;
 
@@ -120,6 +125,43 @@ int dcte_energy_map_device(dcte_ctx *ctx, int device, const void *d_px,
                            int in_row0, int in_rows, int y0, int y1, int n,
                            float edges, float textures, int semantics, float *d_out,
                            long long out_stride, void *stream);
+
+/* ---- seam carving support --------------------------------
+ * After the initial map, liblqr carves one seam at a time and re-evaluates
+ * the callback (src/render.c:134-157) only around the removed seam
+ * (update_emap, during lqr_carver_resize at src/render.c:377) [liblqr,
+ * unverified].  With the frame and its map resident in HBM this is one call
+ * per seam:
+ *
+ * dcte_seam_carve_device: removes pixel d_seam[y] from every row y of the
+ *   w x h frame (d_px) -> the (w-1) x h frame d_px_out, and writes the map of
+ *   that frame to d_map_out: pixels whose window lies on one side of the
+ *   seam are moved from d_map (the map of d_px), the <= N-1+drift pixels per
+ *   row whose window straddles it are recomputed -- exactly the values
+ *   dcte_energy_map gives for d_px_out (same fp32 passes, same refinement).
+ *   d_seam: h device ints in [0, w) (values outside are clamped).  Buffers
+ *   must not overlap (ping-pong two frame/map pairs).  Stream-ordered. */
+int dcte_seam_carve_device(dcte_ctx *ctx, int device, const void *d_px, long long rowstride,
+                           int w, int h, int bpp, const int *d_seam, const float *d_map,
+                           long long map_stride, void *d_px_out, long long out_rowstride,
+                           float *d_map_out, long long map_out_stride, int n, float edges,
+                           float textures, int semantics, void *stream);
+
+/* Energies at listed pixels -- the batched form of the per-pixel callback
+ * (one dct_pixel_energy per point, src/render.c:134-157), for a carver-side
+ * hook that re-evaluates a set of pixels at once.  xy: count (x, y) pairs;
+ * out[k] = energy of pixel (xy[2k], xy[2k+1]) of the w x h frame, equal to
+ * that pixel of dcte_energy_map.  Host version: the frame and points are
+ * copied to the first device; coordinates outside the frame are
+ * DCTE_EINVAL.  Device version: whole frame resident, coordinates clamped,
+ * stream-ordered. */
+int dcte_energy_points(dcte_ctx *ctx, const uint8_t *px, int w, int h, int bpp,
+                       size_t rowstride, const int *xy, int count, int n, float edges,
+                       float textures, int semantics, float *out);
+int dcte_energy_points_device(dcte_ctx *ctx, int device, const void *d_px, long long rowstride,
+                              int w, int h, int bpp, const int *d_xy, int count, int n,
+                              float edges, float textures, int semantics, float *d_out,
+                              void *stream);
 
 /* ---- energy image as 8-bit grey ----------------------
  * DCTE_NORM_PREVIEW: normalize_image (src/render.c:81-109, DOUBLE2GUCHAR of

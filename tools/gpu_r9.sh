@@ -1,0 +1,13 @@
+#!/bin/bash
+# seam/points tests, the full GPU suite, then the host-path timing
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+OUT="$GRAFT_REPO_ROOT/gpurun_out"; mkdir -p "$OUT"
+timeout -k 10 300 python -m pytest tests/test_seam.py -m gpu -q -x -p no:cacheprovider > "$OUT/pytest_seam.log" 2>&1
+rc=$?; echo "seam exit $rc" >> "$OUT/pytest_seam.log"; tail -25 "$OUT/pytest_seam.log"
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1
+rc=$?; echo "pytest exit $rc" >> "$OUT/pytest_gpu.log"; tail -5 "$OUT/pytest_gpu.log"
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python tools/host_path.py --size 16384 > "$OUT/host_path.jsonl" 2> "$OUT/host_path.err"
+rc=$?; cat "$OUT/host_path.jsonl"; tail -3 "$OUT/host_path.err"; exit $rc

@@ -49,12 +49,18 @@ def main():
     mpx = S * S / 1e6
     res = []
     with dctenergy.Context(ngpus=1) as ctx:
-        for name, src, dst in (("pageable", px_np, out_np), ("pinned", px_pin.numpy(), out_pin.numpy())):
+        cases = (("pageable, DCTE_OPT_PIN_HOST=0 (runtime-staged copies)", px_np, out_np, 0),
+                 ("pageable, page-locked per call (default)", px_np, out_np, 64),
+                 ("caller-pinned buffers", px_pin.numpy(), out_pin.numpy(), 64))
+        for name, src, dst, pin in cases:
+            ctx.set_option(dctenergy.DCTE_OPT_PIN_HOST, pin)
             med, best = timed(lambda: ctx.energy_map(src, a.n, 0.3, 0.7, out=dst), a.iters)
             res.append({"case": f"dcte_energy_map host->host ({name})", "ms": round(med * 1e3, 2),
                         "best_ms": round(best * 1e3, 2), "mpx_s": round(mpx / med, 1)})
+        ctx.set_option(dctenergy.DCTE_OPT_PIN_HOST, 64)
         med, best = timed(lambda: ctx.energy_image_u8(px_np, a.n, 0.3, 0.7), a.iters)
-        res.append({"case": "dcte_energy_image_u8 host->host (pageable)", "ms": round(med * 1e3, 2),
+        res.append({"case": "dcte_energy_image_u8 host->host (pageable, fresh output array per call)",
+                    "ms": round(med * 1e3, 2),
                     "mpx_s": round(mpx / med, 1)})
     # bare copy rates of the same bytes (torch, same stream semantics)
     for name, fn, nbytes in (
