@@ -40,27 +40,115 @@ __device__ __forceinline__ void seam_span(const int* __restrict__ seam, int w, i
     }
 }
 
-// new frame + the map pixels that only move: one thread per new pixel
-template <int BPP>
-__global__ __launch_bounds__(256) void dcte_seam_shift(const SeamParams p)
+constexpr unsigned kRawBufFlags = 0x00020000u;   // gfx9 raw buffer dword3 (as dcte_map)
+constexpr int kShiftThreads = 256;
+constexpr int kShiftDw = 4;                        // dwords per thread per pass
+
+// 4 bytes at byte offset `off` (any alignment) of a buffer resource: two
+// aligned dword loads + a byte funnel shift (out-of-range dwords read 0)
+__device__ __forceinline__ uint32_t load4(__amdgpu_buffer_rsrc_t r, uint32_t off)
 {
-    const int y = blockIdx.y;
-    const int x = blockIdx.x * 256 + threadIdx.x;
-    const int w1 = p.w - 1;
-    if (x >= w1) return;
-    const int s = clamp_px(p.seam[y], 0, p.w - 1);
-    const int xs = x + (x >= s ? 1 : 0);
-    const uint8_t* src = p.px + (long long)y * p.rowstride + (long long)xs * BPP;
-    uint8_t* dst = p.px_out + (long long)y * p.out_rowstride + (long long)x * BPP;
-#pragma unroll
-    for (int c = 0; c < BPP; c++) dst[c] = src[c];
+    const uint32_t a = off & ~3u, sh = off & 3u;
+    const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(r, (int)a, 0, 0);
+    const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(a + 4u), 0, 0);
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * sh));
+}
+
+// One workgroup per row.  New row bytes [o0, o1) come from old byte
+// b + (b >= s*bpp ? bpp : 0); new map entries x come from old x (left of the
+// recomputed band) or x + 1 (right of it).  INPLACE (px_out == px, same row
+// stride; map likewise): only the part right of the seam moves (o0 = s*bpp),
+// every pass loads all its sources before the barrier and stores after it,
+// and a pass never reads bytes an earlier pass wrote (sources lie at or
+// right of the destinations); the <= 3 unaligned head bytes are loaded first
+// and the <= 3 tail bytes (read as sources by the last dwords) are stored last.
+template <int BPP, bool INPLACE>
+__global__ __launch_bounds__(kShiftThreads) void dcte_seam_shift(const SeamParams p)
+{
+    const int y = blockIdx.x;
+    const int tx = threadIdx.x;
+    const int w = p.w, w1 = w - 1;
+    const int s = clamp_px(p.seam[y], 0, w - 1);
     int lo, hi;
-    seam_span(p.seam, p.w, p.h, p.n, p.sem, y, lo, hi);
+    seam_span(p.seam, w, p.h, p.n, p.sem, y, lo, hi);
     const int HL = halo_left(p.n, p.sem), HR = p.n - 1 - HL;
-    if (x + HR < lo)
-        p.map_out[(long long)y * p.map_out_stride + x] = p.map[(long long)y * p.map_stride + x];
-    else if (min(x - HL, p.w - 2) >= hi)
-        p.map_out[(long long)y * p.map_out_stride + x] = p.map[(long long)y * p.map_stride + x + 1];
+
+    // ---- frame bytes
+    const uintptr_t ib = reinterpret_cast<uintptr_t>(p.px);
+    const uint32_t iofs = (uint32_t)(ib & 3u);
+    // records rounded up to whole dwords: buffer loads are range-checked per
+    // dword, and the aligned dword holding the frame's last byte never
+    // crosses a page, so it is always mapped
+    const uint32_t nrec =
+        (iofs + (uint32_t)((long long)(p.h - 1) * p.rowstride) + (uint32_t)(w * BPP) + 3u) & ~3u;
+    __amdgpu_buffer_rsrc_t in = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(ib - iofs), (short)0, (int)nrec, (int)kRawBufFlags);
+    const uint32_t irow = iofs + (uint32_t)((long long)y * p.rowstride);   // row y in `in`
+    uint8_t* orow = p.px_out + (long long)y * p.out_rowstride;
+    const int sb = s * BPP;
+    const int o0 = INPLACE ? sb : 0, o1 = w1 * BPP;
+    auto src = [&](int b) -> uint32_t { return irow + (uint32_t)(b + (b >= sb ? BPP : 0)); };
+    // aligned dword span [d0, d1) of the destination row, head [o0, d0), tail [d1, o1)
+    const int mis = (int)(reinterpret_cast<uintptr_t>(orow) & 3u);
+    int d0 = o0 + ((4 - ((mis + o0) & 3)) & 3);
+    if (d0 > o1) d0 = o1;
+    int d1 = d0 + ((o1 - d0) & ~3);
+    uint8_t edge_v = 0;                               // one head/tail byte per thread < 6
+    int edge_b = -1;
+    if (tx < 3 && o0 + tx < d0) edge_b = o0 + tx;
+    if (tx >= 3 && tx < 6 && d1 + (tx - 3) < o1) edge_b = d1 + (tx - 3);
+    if (edge_b >= 0) edge_v = (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(in, (int)src(edge_b), 0, 0);
+    for (int base = d0; base < d1; base += 4 * kShiftThreads * kShiftDw) {
+        uint32_t v[kShiftDw];
+#pragma unroll
+        for (int k = 0; k < kShiftDw; k++) {
+            const int b = base + 4 * (tx + k * kShiftThreads);
+            v[k] = 0;
+            if (b < d1) {
+                if (b + 4 <= sb || b >= sb) {
+                    v[k] = load4(in, src(b));
+                } else {                                   // dword straddling the seam
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        v[k] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(in, (int)src(b + j), 0, 0) << (8 * j);
+                }
+            }
+        }
+        if constexpr (INPLACE) __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kShiftDw; k++) {
+            const int b = base + 4 * (tx + k * kShiftThreads);
+            if (b < d1) *reinterpret_cast<uint32_t*>(orow + b) = v[k];
+        }
+    }
+
+    // ---- map: rows of floats (4-byte aligned)
+    const float* mrow = p.map + (long long)y * p.map_stride;
+    float* nrow = p.map_out + (long long)y * p.map_out_stride;
+    // left part [0, lo - HR) keeps x; right part [r0, w1) takes x + 1
+    const int lend = max(0, min(w1, lo - HR));
+    int r0 = hi + HL;                                  // first x with min(x - HL, w - 2) >= hi
+    if (hi > w - 2) r0 = w1;
+    r0 = max(r0, 0);
+    if constexpr (!INPLACE) {
+        for (int x = tx; x < lend; x += kShiftThreads) nrow[x] = mrow[x];
+    }
+    for (int base = r0; base < w1; base += kShiftThreads * kShiftDw) {
+        float v[kShiftDw];
+#pragma unroll
+        for (int k = 0; k < kShiftDw; k++) {
+            const int x = base + tx + k * kShiftThreads;
+            v[k] = x < w1 ? mrow[x + 1] : 0.0f;
+        }
+        if constexpr (INPLACE) __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kShiftDw; k++) {
+            const int x = base + tx + k * kShiftThreads;
+            if (x < w1) nrow[x] = v[k];
+        }
+    }
+    if constexpr (INPLACE) __syncthreads();
+    if (edge_b >= 0) orow[edge_b] = edge_v;
 }
 
 __device__ __forceinline__ void emit_pixel(const SeamParams& p, float mt, float me, float* dst,
@@ -139,13 +227,21 @@ static hipError_t launch_points_n(const SeamParams& p, hipStream_t s)
 hipError_t launch_seam_carve(const SeamParams& p, hipStream_t s)
 {
     if (p.w < 2 || p.h < 1) return hipErrorInvalidValue;
-    dim3 grid((p.w - 1 + 255) / 256, p.h), block(256);
+    dim3 grid(p.h), block(kShiftThreads);
+    const bool inplace = p.px_out == p.px && p.out_rowstride == p.rowstride &&
+                         p.map_out == p.map && p.map_out_stride == p.map_stride;
+#define DCTE_SHIFT(B)                                                                        \
+    case B:                                                                                  \
+        if (inplace) hipLaunchKernelGGL((dcte_seam_shift<B, true>), grid, block, 0, s, p);  \
+        else hipLaunchKernelGGL((dcte_seam_shift<B, false>), grid, block, 0, s, p);         \
+        break;
     switch (p.bpp) {
-    case 1: hipLaunchKernelGGL(dcte_seam_shift<1>, grid, block, 0, s, p); break;
-    case 3: hipLaunchKernelGGL(dcte_seam_shift<3>, grid, block, 0, s, p); break;
-    case 4: hipLaunchKernelGGL(dcte_seam_shift<4>, grid, block, 0, s, p); break;
+        DCTE_SHIFT(1)
+        DCTE_SHIFT(3)
+        DCTE_SHIFT(4)
     default: return hipErrorInvalidValue;
     }
+#undef DCTE_SHIFT
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     switch (p.n) {

@@ -139,8 +139,11 @@ int dcte_energy_map_device(dcte_ctx *ctx, int device, const void *d_px,
  *   seam are moved from d_map (the map of d_px), the <= N-1+drift pixels per
  *   row whose window straddles it are recomputed -- exactly the values
  *   dcte_energy_map gives for d_px_out (same fp32 passes, same refinement).
- *   d_seam: h device ints in [0, w) (values outside are clamped).  Buffers
- *   must not overlap (ping-pong two frame/map pairs).  Stream-ordered. */
+ *   d_seam: h device ints in [0, w) (values outside are clamped).
+ *   In place: d_px_out == d_px with the same row stride AND d_map_out ==
+ *   d_map with the same stride -- only the part right of the seam moves (the
+ *   frame keeps its row stride, one pixel narrower).  Otherwise the output
+ *   buffers must not overlap the inputs.  Stream-ordered. */
 int dcte_seam_carve_device(dcte_ctx *ctx, int device, const void *d_px, long long rowstride,
                            int w, int h, int bpp, const int *d_seam, const float *d_map,
                            long long map_stride, void *d_px_out, long long out_rowstride,

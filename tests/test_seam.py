@@ -34,9 +34,10 @@ def _seams(seed, steps):
     return [gen] * steps
 
 
-def _carve_run(ctx, img, n, e, t, sem, seams):
+def _carve_run(ctx, img, n, e, t, sem, seams, inplace=False):
     """Carve seams one by one on the device; check every step.  seams: arrays,
-    or callables (k, h, width) -> array."""
+    or callables (k, h, width) -> array.  inplace: the carved frame and map
+    stay in the original buffers (narrowing views, original row strides)."""
     torch = _torch()
     dev = torch.device("cuda")
     cur = torch.from_numpy(img).to(dev)
@@ -48,8 +49,12 @@ def _carve_run(ctx, img, n, e, t, sem, seams):
         if callable(s):
             s = s(k, h, cur.shape[1])
         s = np.clip(s, 0, cur.shape[1] - 1).astype(np.int32)
-        nxt = torch.empty((h, cur.shape[1] - 1) + tuple(cur.shape[2:]), dtype=torch.uint8, device=dev)
-        nmap = torch.full((h, cur.shape[1] - 1), np.nan, dtype=torch.float32, device=dev)
+        if inplace:
+            nxt, nmap = cur[:, :cur.shape[1] - 1], emap[:, :cur.shape[1] - 1]
+        else:
+            nxt = torch.empty((h, cur.shape[1] - 1) + tuple(cur.shape[2:]), dtype=torch.uint8,
+                              device=dev)
+            nmap = torch.full((h, cur.shape[1] - 1), np.nan, dtype=torch.float32, device=dev)
         ctx.seam_carve_tensor(cur, torch.from_numpy(s).to(dev), emap, nxt, nmap, n, e, t,
                               semantics=sem)
         host = carve(host, s)
@@ -66,13 +71,13 @@ def _carve_run(ctx, img, n, e, t, sem, seams):
     return host, emap.cpu().numpy()
 
 
+@pytest.mark.parametrize("inplace", [False, True], ids=["copy", "inplace"])
 @pytest.mark.parametrize("n", [2, 4, 8, 16])
 @pytest.mark.parametrize("sem,name", [(0, "natural_rgb_73x59.npy"), (0, "natural_grey_200x120.npy"),
                                       (1, "rgba_45x38.npy"), (1, "natural_rgb_73x59.npy")])
-def test_carve_updates_equal_full_map(ctx, n, sem, name):
+def test_carve_updates_equal_full_map(ctx, n, sem, name, inplace):
     img = load_input(name)
-    h, w = img.shape[:2]
-    host, E = _carve_run(ctx, img, n, 0.15, 0.85, sem, _seams(n, 12))
+    host, E = _carve_run(ctx, img, n, 0.15, 0.85, sem, _seams(n, 12), inplace)
     ref = _oracle(host, n, 0.15, 0.85, sem)
     assert within_tol(E, ref).all()
 
@@ -97,6 +102,8 @@ def test_carve_to_narrow_frames(ctx):
     seams = [np.full(h, k % 3, np.int32) for k in range(8)]
     host, E = _carve_run(ctx, img, 8, 0.3, 0.7, 0, seams)
     assert host.shape[1] == 2
+    host2, E2 = _carve_run(ctx, img, 8, 0.3, 0.7, 0, seams, inplace=True)
+    assert np.array_equal(host2, host) and np.array_equal(E2, E)
     assert within_tol(E, O.energy_map(host, 8, 0.3, 0.7)).all()
 
 
