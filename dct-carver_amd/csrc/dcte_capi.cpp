@@ -31,6 +31,11 @@ struct FixScratch {
     size_t cap = 0;
 };
 
+struct DpScratch {                 // seam DP (dcte_dp.hip), per stream
+    void* buf = nullptr;
+    size_t cap = 0;
+};
+
 struct Device {
     int id = -1;
     hipStream_t stream = nullptr;  // used by the host entry point
@@ -39,6 +44,7 @@ struct Device {
     float* d_out = nullptr;
     size_t out_cap = 0;
     std::map<hipStream_t, FixScratch> fix;
+    std::map<hipStream_t, DpScratch> dp;
     unsigned* d_keys = nullptr;    // min/max scratch (per device; stream-ordered)
     float* d_minmax = nullptr;
     uint8_t* d_u8 = nullptr;       // u8 staging for the host entry points
@@ -479,6 +485,10 @@ void dcte_destroy(dcte_ctx* ctx)
             if (kv.second.d_count) (void)hipFree(kv.second.d_count);
             if (kv.second.d_list) (void)hipFree(kv.second.d_list);
         }
+        for (auto& kv : d.dp) {
+            (void)hipStreamSynchronize(kv.first);
+            if (kv.second.buf) (void)hipFree(kv.second.buf);
+        }
         if (d.d_in) (void)hipFree(d.d_in);
         if (d.d_out) (void)hipFree(d.d_out);
         if (d.d_keys) (void)hipFree(d.d_keys);
@@ -660,6 +670,79 @@ int dcte_energy_points(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, 
     DCTE_HIP(ctx, hipMemcpyAsync(out, d.d_out, sizeof(float) * (size_t)count,
                                  hipMemcpyDeviceToHost, d.stream));
     return sync_bands(ctx, 1);
+}
+
+int dcte_seam_find_device(dcte_ctx* ctx, int device, const float* d_map, long long map_stride,
+                          int w, int h, int* d_seam, void* stream)
+{
+    if (!ctx) return DCTE_EINVAL;
+    DCTE_ARG(ctx, device >= 0 && device < (int)ctx->devs.size());
+    DCTE_ARG(ctx, d_map && d_seam && w >= 1 && h >= 1 && map_stride >= w);
+    Device& d = ctx->devs[device];
+    hipStream_t s = (hipStream_t)stream;
+    DCTE_HIP(ctx, hipSetDevice(d.id));
+    const int R = dcte::dp_band_rows(), G = dcte::dp_super_bands(), T = dcte::dp_tile_cols();
+    dcte::DpParams p{};
+    p.map = d_map;
+    p.stride = map_stride;
+    p.w = w;
+    p.h = h;
+    p.nb = (h + R - 1) / R;
+    p.ns = (p.nb + G - 1) / G;
+    p.ntiles = (w + T - 1) / T;
+    // scratch: bound | jump | sjump | sx | bx | flags | err | par (bytes last)
+    const size_t W = (size_t)w;
+    const size_t n_bound = (size_t)p.nb * W, n_jump = (size_t)p.nb * W, n_sj = (size_t)p.ns * W;
+    const size_t words = n_bound + n_jump + n_sj + p.ns + p.nb + p.ntiles + 1;
+    const size_t bytes = words * 4 + W * (size_t)h;
+    DpScratch& sc = d.dp[s];
+    if (sc.cap < bytes) {
+        if (sc.buf) DCTE_HIP(ctx, hipFree(sc.buf));
+        sc.buf = nullptr;
+        sc.cap = 0;
+        DCTE_HIP(ctx, hipMalloc(&sc.buf, bytes));
+        sc.cap = bytes;
+    }
+    uint32_t* wbase = static_cast<uint32_t*>(sc.buf);
+    p.bound = reinterpret_cast<float*>(wbase);
+    p.jump = reinterpret_cast<int*>(wbase + n_bound);
+    p.sjump = p.jump + n_jump;
+    p.sx = p.sjump + n_sj;
+    p.bx = p.sx + p.ns;
+    p.flags = reinterpret_cast<unsigned*>(p.bx + p.nb);
+    p.err = p.flags + p.ntiles;
+    p.par = reinterpret_cast<int8_t*>(wbase + words);
+    p.seam = d_seam;
+    DCTE_HIP(ctx, hipMemsetAsync(p.flags, 0, sizeof(unsigned) * ((size_t)p.ntiles + 1), s));
+    DCTE_HIP(ctx, dcte::launch_seam_find(p, s));
+    return DCTE_OK;
+}
+
+int dcte_seam_find(dcte_ctx* ctx, const float* map, int w, int h, int* seam)
+{
+    if (!ctx) return DCTE_EINVAL;
+    DCTE_ARG(ctx, map && seam && w >= 1 && h >= 1);
+    Device& d = ctx->devs[0];
+    int rc = ensure_stream(ctx, d);
+    if (rc) return rc;
+    const size_t mbytes = sizeof(float) * (size_t)w * (size_t)h;
+    rc = ensure_buf(ctx, (void**)&d.d_out, &d.out_cap, mbytes + sizeof(int) * (size_t)h);
+    if (rc) return rc;
+    int* d_seam = reinterpret_cast<int*>(reinterpret_cast<uint8_t*>(d.d_out) + mbytes);
+    DCTE_HIP(ctx, hipMemcpyAsync(d.d_out, map, mbytes, hipMemcpyHostToDevice, d.stream));
+    rc = dcte_seam_find_device(ctx, 0, d.d_out, w, w, h, d_seam, d.stream);
+    if (rc) {
+        drain(ctx, 1);
+        return rc;
+    }
+    DCTE_HIP(ctx, hipMemcpyAsync(seam, d_seam, sizeof(int) * (size_t)h, hipMemcpyDeviceToHost,
+                                 d.stream));
+    DCTE_HIP(ctx, hipStreamSynchronize(d.stream));
+    if (h > 0 && seam[0] < 0) {
+        ctx->last_error = "seam search timed out waiting for a neighbour tile";
+        return DCTE_EHIP;
+    }
+    return DCTE_OK;
 }
 
 int dcte_energy_map(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride,

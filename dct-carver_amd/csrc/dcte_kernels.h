@@ -67,11 +67,32 @@ struct SeamParams {
     unsigned fix_cap;
 };
 
+// Minimum-energy seam (dcte_dp.hip): scratch sized by the launcher.
+struct DpParams {
+    const float* map;        // w x h energies
+    long long stride;        // floats
+    int w, h;
+    int nb, ns, ntiles;      // bands (dp_band_rows rows), super-bands, column tiles
+    float* bound;            // nb x w: cumulative energy at each band's last row
+    int8_t* par;             // h x w: parent offset -1 / 0 / +1 (rows >= 1)
+    int* jump;               // nb x w
+    int* sjump;              // ns x w
+    int* sx;                 // ns
+    int* bx;                 // nb
+    unsigned* flags;         // ntiles, zeroed before the launch
+    unsigned* err;           // 1, zeroed before the launch
+    int* seam;               // h: column removed per row (-1 everywhere on failure)
+};
+
 // host-side launchers (dcte_kernels.hip)
 hipError_t launch_map(int n, int bpp, int sem, const MapParams& p, hipStream_t s);
 hipError_t launch_fix(const FixParams& p, hipStream_t s);
 hipError_t launch_seam_carve(const SeamParams& p, hipStream_t s);
 hipError_t launch_points(const SeamParams& p, hipStream_t s);
+hipError_t launch_seam_find(const DpParams& p, hipStream_t s);
+int dp_tile_cols();
+int dp_band_rows();
+int dp_super_bands();
 
 // geometry the launcher uses (exported for tests / bench)
 int map_tile_w(int n);

@@ -41,7 +41,7 @@ EXPORTS = ("dcte_abi_version", "dcte_device_count", "dcte_create", "dcte_destroy
            "dcte_energy_map_device", "dcte_last_refined", "dcte_profile_read", "dcte_strerror",
            "dcte_last_error", "dcte_normalize_u8", "dcte_energy_image_u8", "dcte_minmax_device",
            "dcte_normalize_u8_device", "dcte_seam_carve_device", "dcte_energy_points",
-           "dcte_energy_points_device")
+           "dcte_energy_points_device", "dcte_seam_find_device", "dcte_seam_find")
 
 _lib = None
 
@@ -129,6 +129,10 @@ def lib():
     L.dcte_energy_points.argtypes = [vp, vp, i, i, i, ctypes.c_size_t, vp, i, i, f, f, i, vp]
     L.dcte_energy_points_device.restype = i
     L.dcte_energy_points_device.argtypes = [vp, i, vp, ll, i, i, i, vp, i, i, f, f, i, vp, vp]
+    L.dcte_seam_find_device.restype = i
+    L.dcte_seam_find_device.argtypes = [vp, i, vp, ll, i, i, vp, vp]
+    L.dcte_seam_find.restype = i
+    L.dcte_seam_find.argtypes = [vp, vp, i, i, vp]
     L.dcte_strerror.restype = ctypes.c_char_p
     L.dcte_strerror.argtypes = [ctypes.c_int]
     L.dcte_last_error.restype = ctypes.c_char_p
@@ -345,6 +349,30 @@ class Context:
             ctypes.c_void_p(emap_out.data_ptr()), emap_out.stride(0), n, edges, textures,
             semantics, ctypes.c_void_p(stream)))
         return px_out, emap_out
+
+    # -- minimum-energy seam
+    def seam_find(self, E):
+        """Vertical seam (column per row) of an HxW float32 host energy map."""
+        E = np.ascontiguousarray(E, dtype=np.float32)
+        h, w = E.shape
+        seam = np.empty(h, np.int32)
+        self._check(lib().dcte_seam_find(self._h, E.ctypes.data, w, h, seam.ctypes.data))
+        return seam
+
+    def seam_find_tensor(self, emap, seam, stream=None, device=0):
+        """Device version: emap float32 [H, >=W] (row stride emap.stride(0)), seam int32 [H]."""
+        import torch
+        if emap.dtype != torch.float32 or seam.dtype != torch.int32 or not seam.is_contiguous():
+            raise TypeError("emap float32, seam contiguous int32")
+        h, w = emap.shape
+        if seam.numel() != h or emap.stride(1) != 1:
+            raise ValueError("seam needs h entries; map rows dense")
+        if stream is None:
+            stream = torch.cuda.current_stream(emap.device).cuda_stream
+        self._check(lib().dcte_seam_find_device(
+            self._h, device, ctypes.c_void_p(emap.data_ptr()), emap.stride(0), w, h,
+            ctypes.c_void_p(seam.data_ptr()), ctypes.c_void_p(stream)))
+        return seam
 
 
 __all__ = ["Context", "DcteError", "lib", "device_count", "LIB_PATH", "EXPORTS",

@@ -166,6 +166,22 @@ int dcte_energy_points_device(dcte_ctx *ctx, int device, const void *d_px, long 
                               float edges, float textures, int semantics, float *d_out,
                               void *stream);
 
+/* ---- minimum-energy seam ---------------------------------
+ * liblqr's cumulative energy for the reference's carver configuration
+ * (lqr_carver_init(carver, 1, 0), src/render.c:313: delta_x 1, rigidity 0)
+ * [liblqr, unverified]: M[0] = E[0], M[y][x] = E[y][x] + min(M[y-1][x-1..x+1]),
+ * float arithmetic, leftmost minimum on ties; the seam ends at the leftmost
+ * minimum of the last row.  seam[y] = column to remove in row y (feed it to
+ * dcte_seam_carve_device).  Vertical seams of a w x h map; for horizontal
+ * seams pass the transposed map.
+ * Device version: stream-ordered; if the search fails internally (a tile
+ * waited ~1 s for a neighbour) d_seam is filled with -1.
+ * Host version: map is w*h floats (row stride w); returns DCTE_EHIP on that
+ * failure. */
+int dcte_seam_find_device(dcte_ctx *ctx, int device, const float *d_map, long long map_stride,
+                          int w, int h, int *d_seam, void *stream);
+int dcte_seam_find(dcte_ctx *ctx, const float *map, int w, int h, int *seam);
+
 /* ---- energy image as 8-bit grey ----------------------
  * DCTE_NORM_PREVIEW: normalize_image (src/render.c:81-109, DOUBLE2GUCHAR of
  *   src/render.h:6): ROUND(255*(E-min)/(max-min)) in double, replicated to

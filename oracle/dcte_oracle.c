@@ -17,20 +17,24 @@
  *                  SURVEY.md §8a-a2)
  *   window gather src/render.c:122-132 (clamp_offset_to_border) and
  *                 src/render.c:134-152 (dct_pixel_energy): data[dx][dy]
- *   dispatch      src/dct.c:93-110 (dctNxN): N=2,4 -> ddct2d, 8 -> ddct8x8s,
+ *   dispatch      src/dct.c:77-94 (dctNxN): N=2,4 -> ddct2d, 8 -> ddct8x8s,
  *                 16 -> ddct16x16s
  *   ddct8x8s      src/fft2d/shrtdct.c:55-117 (forward branch, isgn<0)
  *   ddct16x16s    src/fft2d/shrtdct.c:231-386 (forward branch)
  *   ddct2d        src/fft2d/fftsg2d.c:566-627 -> ddct src/fft2d/fftsg.c:349-402,
  *                 cftx020 :3211, dctsub :3274, makect :724 (N=2,4 only)
- *   weighted max  src/dct.c:112-126 (weighted_max_dct_correlation) with the
- *                 edge-atom LUTs src/dct.c:26-59 (edges = (0,1),(1,0))
+ *   weighted max  src/dct.c:96-110 (weighted_max_dct_correlation) with the
+ *                 edge-atom test src/dct.c:56-73 (edges = (0,1),(1,0))
  *   preview       the GTK preview's second energy semantics,
  *                 dct_energy_preview / dct_energy_preview_rows /
  *                 convert_row_to_luminance (src/render.c:31-79, :421-479):
  *                 u8 luma RGB2LUMINANCE (src/render.h:5), window rows and
  *                 columns -(c-1)..N-c with c = CENTER_ROW(N) = (N-1)/2
  *                 (src/dct.h:8-9), stored data[dy][dx]
+ *
+ *   seam DP       liblqr's cumulative energy for the carver configured at
+ *                 src/render.c:313 (lqr_carver_init(carver, 1, 0): delta_x 1,
+ *                 rigidity 0) and its seam backtrack [liblqr, unverified]
  *
  * Compile with -ffp-contract=off (the Makefile does): the reference is plain
  * C on x86-64 where gcc emits no fused multiply-adds.
@@ -397,4 +401,60 @@ int orc_max_threads(void)
 #else
     return 1;
 #endif
+}
+
+/* ---- seam DP [liblqr, unverified] -------------------------
+ * The carver is set up with delta_x = 1 and rigidity 0 (src/render.c:313),
+ * so the cumulative energy is the classic 3-neighbour recursion, in float
+ * (gfloat) arithmetic:
+ *     M[0][x] = E[0][x]
+ *     M[y][x] = E[y][x] + min(M[y-1][x-1], M[y-1][x], M[y-1][x+1])
+ * with candidates scanned left to right and replaced only on a strictly
+ * smaller value (the leftmost minimum wins; out-of-frame candidates do not
+ * exist).  The seam ends at the leftmost minimum of the last row and follows
+ * the recorded parents up.  seam[y] = column removed in row y.
+ * M may be NULL; returns 0, or -1 on bad sizes. */
+int orc_seam_find(const float *E, long long stride, int w, int h, int *seam, float *M)
+{
+    if (w <= 0 || h <= 0 || stride < w) return -1;
+    float *m = (float *)malloc(sizeof(float) * (size_t)w * 2);
+    signed char *par = (signed char *)malloc((size_t)w * (size_t)h);
+    if (!m || !par) {
+        free(m);
+        free(par);
+        return -1;
+    }
+    float *prev = m, *cur = m + w;
+    for (int x = 0; x < w; x++) prev[x] = E[x];
+    if (M) for (int x = 0; x < w; x++) M[x] = prev[x];
+    for (int y = 1; y < h; y++) {
+        const float *e = E + (size_t)y * stride;
+        for (int x = 0; x < w; x++) {
+            int lo = x > 0 ? x - 1 : 0, hi = x < w - 1 ? x + 1 : w - 1;
+            float best = prev[lo];
+            int arg = lo;
+            for (int c = lo + 1; c <= hi; c++)
+                if (prev[c] < best) {
+                    best = prev[c];
+                    arg = c;
+                }
+            cur[x] = e[x] + best;
+            par[(size_t)y * w + x] = (signed char)(arg - x);
+        }
+        if (M) for (int x = 0; x < w; x++) M[(size_t)y * w + x] = cur[x];
+        float *t = prev;
+        prev = cur;
+        cur = t;
+    }
+    int x = 0;
+    for (int c = 1; c < w; c++)
+        if (prev[c] < prev[x]) x = c;
+    seam[h - 1] = x;
+    for (int y = h - 1; y > 0; y--) {
+        x += par[(size_t)y * w + x];
+        seam[y - 1] = x;
+    }
+    free(m);
+    free(par);
+    return 0;
 }

@@ -62,6 +62,9 @@ def lib():
                                            ctypes.c_size_t, ctypes.c_int, ctypes.c_float,
                                            ctypes.c_float, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_int, _f32p]
+        L.orc_seam_find.restype = ctypes.c_int
+        L.orc_seam_find.argtypes = [_f32p, ctypes.c_longlong, ctypes.c_int, ctypes.c_int,
+                                    ctypes.POINTER(ctypes.c_int), ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -130,6 +133,20 @@ def preview_map(px, n, edges, textures, y0=0, y1=None, nthreads=1):
     if rc != 0:
         raise ValueError(f"oracle rejected the call (rc={rc})")
     return out
+
+
+def seam_find(E, with_m=False):
+    """liblqr-style minimum vertical seam of an HxW float32 energy map
+    (delta_x 1, rigidity 0; leftmost minimum on ties) [liblqr, unverified]."""
+    E = np.ascontiguousarray(E, dtype=np.float32)
+    h, w = E.shape
+    seam = np.empty(h, np.int32)
+    M = np.empty((h, w), np.float32) if with_m else None
+    rc = lib().orc_seam_find(_ptr(E, _f32p), w, w, h, seam.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                             M.ctypes.data if with_m else None)
+    if rc != 0:
+        raise ValueError("oracle rejected the map")
+    return (seam, M) if with_m else seam
 
 
 def window_energy(win, edges, textures):

@@ -1,0 +1,112 @@
+"""GPU: minimum-energy seam (dcte_seam_find[_device]) against
+the oracle's restatement of liblqr's recursion (bit-identical: same float
+adds, same leftmost-minimum rule) [liblqr, unverified], and the whole carve
+loop map -> seam -> carve on the device against the CPU loop."""
+import numpy as np
+import pytest
+
+import dctenergy
+import oracle_py as O
+from golden_util import load_input
+from seam_util import carve
+
+pytestmark = pytest.mark.gpu
+
+
+def _maps(h, w, kind, seed):
+    rng = np.random.default_rng(seed)
+    if kind == "uniform":
+        return rng.random((h, w), dtype=np.float32)
+    if kind == "ties":
+        return rng.integers(0, 3, (h, w)).astype(np.float32)
+    if kind == "flat":
+        return np.ones((h, w), np.float32)
+    # a cheap valley that wanders across tile borders
+    x = np.arange(w)[None, :]
+    c = (w / 2 + (w / 3) * np.sin(np.arange(h)[:, None] / 37.0))
+    return (np.abs(x - c) / w + 0.01 * rng.random((h, w))).astype(np.float32)
+
+
+SHAPES = [(1, 1), (1, 5), (7, 1), (31, 64), (33, 65), (100, 129), (257, 300), (64, 1000),
+          (1000, 77), (129, 4097)]
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: f"{s[0]}x{s[1]}")
+@pytest.mark.parametrize("kind", ["uniform", "ties", "flat", "valley"])
+def test_seam_matches_oracle(ctx, shape, kind):
+    h, w = shape
+    E = _maps(h, w, kind, h * 7 + w)
+    got = ctx.seam_find(E)
+    assert np.array_equal(got, O.seam_find(E))
+
+
+def test_seam_device_strided_and_large(ctx):
+    import torch
+    h, w = 4096, 4096
+    E = _maps(h, w, "valley", 1)
+    buf = torch.full((h, w + 40), np.nan, dtype=torch.float32, device="cuda")
+    buf[:, :w] = torch.from_numpy(E).cuda()
+    seam = torch.empty(h, dtype=torch.int32, device="cuda")
+    ctx.seam_find_tensor(buf[:, :w], seam)
+    torch.cuda.synchronize()
+    assert np.array_equal(seam.cpu().numpy(), O.seam_find(E))
+
+
+def test_seam_bad_arguments(ctx):
+    L = dctenergy.lib()
+    seam = np.empty(4, np.int32)
+    E = np.zeros((4, 4), np.float32)
+    assert L.dcte_seam_find(ctx._h, E.ctypes.data, 0, 4, seam.ctypes.data) == dctenergy.DCTE_EINVAL
+    assert L.dcte_seam_find(ctx._h, None, 4, 4, seam.ctypes.data) == dctenergy.DCTE_EINVAL
+
+
+def _gpu_loop(ctx, img, n, e, t, steps):
+    """map -> (seam -> carve in place) x steps, all on the device."""
+    import torch
+    cur = torch.from_numpy(img).cuda()
+    h, w = img.shape[:2]
+    emap = torch.empty((h, w), dtype=torch.float32, device="cuda")
+    ctx.energy_map_tensor(cur, emap, n, e, t)
+    seam = torch.empty(h, dtype=torch.int32, device="cuda")
+    seams, maps = [], []
+    for k in range(steps):
+        wk = w - k
+        maps.append(emap[:, :wk].cpu().numpy())
+        ctx.seam_find_tensor(emap[:, :wk], seam)
+        ctx.seam_carve_tensor(cur[:, :wk], seam, emap[:, :wk], cur[:, :wk - 1], emap[:, :wk - 1],
+                              n, e, t)
+        seams.append(seam.cpu().numpy().copy())
+    torch.cuda.synchronize()
+    return seams, maps, cur[:, :w - steps].cpu().numpy(), emap[:, :w - steps].cpu().numpy()
+
+
+@pytest.mark.parametrize("n", [4, 8, 16])
+def test_carve_loop_refined_equals_cpu_reference_loop(ctx, n):
+    """With every pixel refined (the reference's own arithmetic) the device
+    loop reproduces the CPU loop exactly: same seams, frame and energies."""
+    img = load_input("wilber_rgb_74x59.npy")
+    ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, 1.0)
+    try:
+        seams, _, frame, E = _gpu_loop(ctx, img, n, 0.3, 0.7, 10)
+    finally:
+        ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, 4e-6)
+    host = img
+    for k in range(10):
+        ref_seam = O.seam_find(O.energy_map(host, n, 0.3, 0.7))
+        assert np.array_equal(seams[k], ref_seam), f"seam {k}"
+        host = carve(host, ref_seam)
+    assert np.array_equal(frame, host)
+    assert np.array_equal(E, O.energy_map(host, n, 0.3, 0.7))
+
+
+def test_carve_loop_default_mode(ctx):
+    """Default (fast fp32 map): each device seam is the oracle's seam of the
+    device map it was found on."""
+    img = load_input("natural_rgb_97x41.npy")
+    seams, maps, frame, _ = _gpu_loop(ctx, img, 8, 0.5, 0.5, 12)
+    for k, (s, m) in enumerate(zip(seams, maps)):
+        assert np.array_equal(s, O.seam_find(m)), f"seam {k}"
+    host = img
+    for s in seams:
+        host = carve(host, s)
+    assert np.array_equal(frame, host)

@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--seams", type=int, default=20)
     ap.add_argument("--bpp", type=int, default=3)
     ap.add_argument("--inplace", action="store_true")
+    ap.add_argument("--find", action="store_true",
+                    help="full carve loop: each seam found on the device (dcte_seam_find_device)")
     a = ap.parse_args()
     import torch
     import dctenergy
@@ -43,11 +45,17 @@ def main():
             seams.append(s.cuda())
         w = S
 
+        found = torch.empty(S, dtype=torch.int32, device="cuda")
+
         def step(k):
             nonlocal w
             i, o = k & 1, (k + 1) & 1
             src, dst = px[i][:, :w], px[o][:, :w - 1]
-            ctx.seam_carve_tensor(src, seams[k], em[i][:, :w], dst, em[o][:, :w - 1], n, 0.3, 0.7)
+            seam = seams[k]
+            if a.find:
+                ctx.seam_find_tensor(em[i][:, :w], found)
+                seam = found
+            ctx.seam_carve_tensor(src, seam, em[i][:, :w], dst, em[o][:, :w - 1], n, 0.3, 0.7)
             w -= 1
 
         for k in range(2):                # warm-up
@@ -62,7 +70,7 @@ def main():
         ms = t0.elapsed_time(t1) / a.seams
     # copy: every pixel read + written; in place: the right part (half on average)
     bytes_per_seam = 2 * (a.bpp + 4) * S * S // (2 if a.inplace else 1)
-    print(json.dumps({"tool": "seam_bench", "size": S, "n": n, "bpp": a.bpp, "seams": a.seams, "inplace": a.inplace,
+    print(json.dumps({"tool": "seam_bench", "size": S, "n": n, "bpp": a.bpp, "seams": a.seams, "inplace": a.inplace, "find": a.find,
                       "ms_per_seam": round(ms, 4),
                       "compaction_GB_s": round(bytes_per_seam / ms / 1e6, 1),
                       "algorithmic_bytes_per_seam": bytes_per_seam}), flush=True)
