@@ -34,6 +34,12 @@ struct FixScratch {
 struct DpScratch {                 // seam DP (dcte_dp.hip), per stream
     void* buf = nullptr;
     size_t cap = 0;
+    // hand-off words live in a buffer of their own that never holds anything
+    // else: every word in it is zero or tagged with an earlier call's epoch
+    void* xbuf = nullptr;
+    size_t xcap = 0;
+    unsigned epoch = 0;            // hand-off tag of the last call
+    int max_tiles = -1;            // co-resident DP tiles on this device
 };
 
 struct Device {
@@ -488,6 +494,7 @@ void dcte_destroy(dcte_ctx* ctx)
         for (auto& kv : d.dp) {
             (void)hipStreamSynchronize(kv.first);
             if (kv.second.buf) (void)hipFree(kv.second.buf);
+            if (kv.second.xbuf) (void)hipFree(kv.second.xbuf);
         }
         if (d.d_in) (void)hipFree(d.d_in);
         if (d.d_out) (void)hipFree(d.d_out);
@@ -687,15 +694,21 @@ int dcte_seam_find_device(dcte_ctx* ctx, int device, const float* d_map, long lo
     p.stride = map_stride;
     p.w = w;
     p.h = h;
-    p.nb = (h + R - 1) / R;
+    p.nb = h > 1 ? (h - 1 + R - 1) / R : 1;  // bands of R rows from row 1 (row 0 seeds M)
     p.ns = (p.nb + G - 1) / G;
     p.ntiles = (w + T - 1) / T;
-    // scratch: bound | jump | sjump | sx | bx | flags | err | par (bytes last)
-    const size_t W = (size_t)w;
-    const size_t n_bound = (size_t)p.nb * W, n_jump = (size_t)p.nb * W, n_sj = (size_t)p.ns * W;
-    const size_t words = n_bound + n_jump + n_sj + p.ns + p.nb + p.ntiles + 1;
-    const size_t bytes = words * 4 + W * (size_t)h;
+    p.pw = (long long)p.ntiles * T;
     DpScratch& sc = d.dp[s];
+    if (sc.max_tiles < 0) sc.max_tiles = dcte::dp_max_tiles(d.id);
+    if (p.ntiles > sc.max_tiles) {
+        ctx->last_error = "seam search: frame too wide for one resident DP tile per column block";
+        return DCTE_EINVAL;
+    }
+    // scratch: jump | sjump | sx | bx | err; xch apart
+    const size_t PW = (size_t)p.pw;
+    const size_t n_x = (size_t)p.nb * PW, n_jump = (size_t)p.nb * PW, n_sj = (size_t)p.ns * PW;
+    const size_t words = n_jump + n_sj + p.ns + p.nb + 1;
+    const size_t bytes = words * 4;
     if (sc.cap < bytes) {
         if (sc.buf) DCTE_HIP(ctx, hipFree(sc.buf));
         sc.buf = nullptr;
@@ -703,17 +716,29 @@ int dcte_seam_find_device(dcte_ctx* ctx, int device, const float* d_map, long lo
         DCTE_HIP(ctx, hipMalloc(&sc.buf, bytes));
         sc.cap = bytes;
     }
+    if (sc.xcap < n_x * 8) {
+        if (sc.xbuf) DCTE_HIP(ctx, hipFree(sc.xbuf));
+        sc.xbuf = nullptr;
+        sc.xcap = 0;
+        DCTE_HIP(ctx, hipMalloc(&sc.xbuf, n_x * 8));
+        sc.xcap = n_x * 8;
+        DCTE_HIP(ctx, hipMemsetAsync(sc.xbuf, 0, sc.xcap, s));
+        sc.epoch = 0;
+    }
+    if (++sc.epoch == 0) {                   // wrapped: clear stale tags
+        DCTE_HIP(ctx, hipMemsetAsync(sc.xbuf, 0, sc.xcap, s));
+        sc.epoch = 1;
+    }
+    p.epoch = sc.epoch;
+    p.xch = static_cast<unsigned long long*>(sc.xbuf);
     uint32_t* wbase = static_cast<uint32_t*>(sc.buf);
-    p.bound = reinterpret_cast<float*>(wbase);
-    p.jump = reinterpret_cast<int*>(wbase + n_bound);
+    p.jump = reinterpret_cast<int*>(wbase);
     p.sjump = p.jump + n_jump;
     p.sx = p.sjump + n_sj;
     p.bx = p.sx + p.ns;
-    p.flags = reinterpret_cast<unsigned*>(p.bx + p.nb);
-    p.err = p.flags + p.ntiles;
-    p.par = reinterpret_cast<int8_t*>(wbase + words);
+    p.err = reinterpret_cast<unsigned*>(p.bx + p.nb);
     p.seam = d_seam;
-    DCTE_HIP(ctx, hipMemsetAsync(p.flags, 0, sizeof(unsigned) * ((size_t)p.ntiles + 1), s));
+    DCTE_HIP(ctx, hipMemsetAsync(p.err, 0, sizeof(unsigned), s));
     DCTE_HIP(ctx, dcte::launch_seam_find(p, s));
     return DCTE_OK;
 }

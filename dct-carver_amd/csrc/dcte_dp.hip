@@ -8,28 +8,46 @@
 // value; the seam ends at the leftmost minimum of the last row and follows
 // the parents up.  The oracle restates it (oracle/dcte_oracle.c
 // orc_seam_find); results here are bit-identical (same float adds, same
-// comparisons).
+// comparisons: min3 gives the same value as the strict-less scan, and the
+// parent is the first candidate equal to it).
 //
-// Rows are sequential, so the DP is latency-bound, not bandwidth-bound.
-// Layout of the work:
-//   dcte_seam_dp     one wave per tile of kDpT = 64 owned columns; each lane
-//                    holds kDpC = 2 columns of a 128-column span (the tile
-//                    plus kDpR = 32 halo columns per side) in registers and
-//                    steps the recursion row by row with two lane shuffles;
-//                    after a band of kDpR rows the halo has decayed exactly
-//                    to the tile, whose last-row M is published to HBM with a
-//                    release flag.  Neighbour tiles wait only on their two
-//                    neighbours' flags (bounded spin; a timeout marks the
-//                    result invalid instead of hanging).  Parent offsets
-//                    (-1/0/+1) of owned cells go to an h x w byte plane.
-//   dcte_seam_jump   per band and column: where the parent chain from the
-//                    band's last row leaves the band (fully parallel).
-//   dcte_seam_sjump  the same over kDpG = 16 bands.
-//   dcte_seam_walk   one workgroup: argmin of the last row, then the chain is
-//                    resolved top-down in three levels (super-bands serially,
-//                    bands per super-band, rows per band), so the dependent
-//                    global loads on the critical path are ~h/512 + 16 + 32
-//                    instead of h.
+// Rows are sequential, so the DP is latency-bound: what matters is the
+// instruction stream ONE wave issues per row (one wave per SIMD issues a VALU
+// op every 4 cycles) and never stalling it on memory.
+//   dcte_seam_dp     one wave per tile of kDpT = 32 C owned columns; lane l
+//                    holds C adjacent columns of a 64 C-column span (the tile
+//                    plus kDpR = 16 C halo columns per side) in registers and
+//                    steps the recursion row by row; the two cross-lane
+//                    neighbours come from DPP wave shifts.  Per row and lane:
+//                    C map loads (buffer loads: scalar row offset + lane
+//                    offset, prefetched 12 rows ahead through a ring of 4-row
+//                    chunks inside a band's straight-line body, so the
+//                    compiler's wait counts stay exact and under vmcnt's 6
+//                    bits), no stores, and for each column one min3, two adds
+//                    (energy + edge bias, then + min), and two compares + two
+//                    selects carrying
+//                    the column where the cell's parent chain entered the band
+//                    (the per-band jump table, free of an extra pass).  Off the
+//                    frame only M[-1] and M[w] matter (as the neighbours of
+//                    columns 0 and w - 1): their energies get +inf added when
+//                    they arrive, off the recursion's critical path, so those
+//                    two columns stay +inf; other off-frame columns hold
+//                    harmless finite values.
+//                    After a band of kDpR rows the halo has decayed exactly to
+//                    the tile.  The tile publishes its last-row M as 8-byte
+//                    {value, epoch} words (write-through, no fences: each word
+//                    carries its own validity) and the halo lanes of its two
+//                    neighbours poll exactly the words they need.  Tiles are
+//                    numbered so that neighbours share an XCD (blockIdx b runs
+//                    on XCD b % 8).
+//   dcte_seam_sjump  the jump table composed over kDpG = 16 bands.
+//   dcte_seam_walk   one workgroup: argmin of the last row, then the chain's
+//                    column at every band's last row, top-down in two levels
+//                    (super-bands serially, then bands per super-band): ~h /
+//                    (16 kDpR) + 16 dependent global loads instead of h.
+//   dcte_seam_rows   one wave per band, all bands at once: the band's rows,
+//                    re-derived from the band's top boundary in a window
+//                    around the chain (nothing per row is kept by the DP).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -37,125 +55,211 @@
 
 namespace dcte {
 
+#ifndef DCTE_DP_C
+#define DCTE_DP_C 2
+#endif
 constexpr int kDpLanes = 64;
-constexpr int kDpC = 2;                              // columns per lane
-constexpr int kDpSpan = kDpLanes * kDpC;             // 128
-constexpr int kDpR = 32;                             // rows per band (= halo)
-constexpr int kDpT = kDpSpan - 2 * kDpR;             // 64 owned columns per wave
+constexpr int kDpC = DCTE_DP_C;                      // columns per lane (1, 2 or 4)
+constexpr int kDpSpan = kDpLanes * kDpC;
+constexpr int kDpR = 16 * kDpC;                      // rows per band (= halo)
+constexpr int kDpT = kDpSpan - 2 * kDpR;             // owned columns per wave
+constexpr int kDpQ = 4;                              // rows per chunk
+#ifndef DCTE_DP_NB
+#define DCTE_DP_NB 4
+#endif
+constexpr int kDpNB = DCTE_DP_NB;                    // chunks in the prefetch ring
 constexpr int kDpG = 16;                             // bands per super-band
-constexpr unsigned kDpSpinLimit = 1u << 24;          // x s_sleep(2): ~1 s
+constexpr int kXcds = 8;
+constexpr unsigned kDpSpinLimit = 1u << 22;          // polls x s_sleep(1): ~0.5 s
+static_assert(kDpC == 1 || kDpC == 2 || kDpC == 4, "C in {1, 2, 4}");
+static_assert(kDpR % kDpQ == 0 && (kDpR / kDpQ) % kDpNB == 0,
+              "a band is a whole number of chunks and of ring turns (static ring slots)");
+static_assert(kDpT >= kDpR, "a halo lies inside one neighbour tile");
 
 int dp_tile_cols() { return kDpT; }
 int dp_band_rows() { return kDpR; }
 int dp_super_bands() { return kDpG; }
 
-__global__ __launch_bounds__(kDpLanes) void dcte_seam_dp(const DpParams p)
+// lane i <- lane i - 1, lane i <- lane i + 1; the lane with no source reads 0
+// (span-edge halo columns only: their values never reach the tile)
+__device__ __forceinline__ int wave_shr1(int v) { return __builtin_amdgcn_mov_dpp(v, 0x138, 0xF, 0xF, true); }
+__device__ __forceinline__ int wave_shl1(int v) { return __builtin_amdgcn_mov_dpp(v, 0x130, 0xF, 0xF, true); }
+
+__global__ __launch_bounds__(kDpLanes) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void dcte_seam_dp(const DpParams p)
 {
-    const int k = blockIdx.x, lane = threadIdx.x;
+    constexpr int C = kDpC;
+    const int per = (p.ntiles + kXcds - 1) / kXcds;
+    const int k = (blockIdx.x % kXcds) * per + blockIdx.x / kXcds;
+    if (k >= p.ntiles) return;
+    const int lane = threadIdx.x;
     const int w = p.w, h = p.h;
+    const long long pw = p.pw;
     const int c0 = k * kDpT;
-    const int xa = c0 - kDpR + lane * kDpC;          // first column of this lane
+    const int xa = c0 - kDpR + lane * C;             // first column of this lane
+    const bool own = lane >= kDpR / C && lane < (kDpR + kDpT) / C;
     const float kInf = __builtin_inff();
-    bool in[kDpC], own[kDpC];
+    const bool left_edge = xa == 0;                  // column 0 is c = 0 of this lane
+    unsigned xoff[C];                                // byte offset of the clamped column
+    bool in[C];
+    float bias[C];                                   // +inf on columns -1 and w, else 0
 #pragma unroll
-    for (int c = 0; c < kDpC; c++) {
+    for (int c = 0; c < C; c++) {
         const int x = xa + c;
         in[c] = x >= 0 && x < w;
-        own[c] = in[c] && x >= c0 && x < c0 + kDpT;
+        xoff[c] = (unsigned)min(max(x, 0), w - 1) * 4u;
+        bias[c] = (x == -1 || x == w) ? kInf : 0.0f;
     }
-    float m[kDpC];
-    for (int j = 0; j < p.nb; j++) {
-        const int y0 = j * kDpR, y1 = min(h, y0 + kDpR);
-        int ys;
-        if (j == 0) {
+    // map rows through a buffer resource based at the current band's first
+    // row (row offsets stay 32-bit); rows past the frame read as 0 and are
+    // never stepped
+    const int rowb = (int)(p.stride * 4);
+    __amdgpu_buffer_rsrc_t ers;
+    auto set_map = [&](int y0) {
+        const long long left = ((long long)(h - 1 - y0) * p.stride + w) * 4;
+        ers = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.map) + (long long)y0 * p.stride,
+                                                (short)0, (int)min(left, 0x7fffffffLL),
+                                                (int)0x00020000);
+    };
+    auto load_row = [&](float (&e)[C], int r) {      // row r of the current map window
 #pragma unroll
-            for (int c = 0; c < kDpC; c++) m[c] = in[c] ? p.map[xa + c] : kInf;
-            ys = 1;
-        } else {
-            if (lane == 0) {
-                unsigned spins = 0;
-                for (;;) {
-                    bool ready = true;
-                    if (k > 0 && __hip_atomic_load(&p.flags[k - 1], __ATOMIC_ACQUIRE,
-                                                   __HIP_MEMORY_SCOPE_AGENT) < (unsigned)j)
-                        ready = false;
-                    if (k + 1 < p.ntiles && __hip_atomic_load(&p.flags[k + 1], __ATOMIC_ACQUIRE,
-                                                              __HIP_MEMORY_SCOPE_AGENT) < (unsigned)j)
-                        ready = false;
-                    if (ready) break;
-                    if (++spins > kDpSpinLimit ||
-                        __hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                        __hip_atomic_fetch_or(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            if (__hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-            const float* b = p.bound + (long long)(j - 1) * w;
+        for (int c = 0; c < C; c++)
+#ifndef DCTE_DP_NOLOAD   // timing experiment only: synthetic energies, no map reads
+            e[c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                 ers, (int)xoff[c], r * rowb, 0));
+#else
+            e[c] = (float)((r * 7 + c + lane) & 15);
+#endif
+    };
+    float m[C];
+    int s[C];
+    auto step = [&](const float (&e)[C]) {
+        float L = __int_as_float(wave_shr1(__float_as_int(m[C - 1])));
+        float R = __int_as_float(wave_shl1(__float_as_int(m[0])));
+        const int sL = wave_shr1(s[C - 1]);
+        const int sR = wave_shl1(s[0]);
+        float nm[C];
+        int ns[C];
 #pragma unroll
-            for (int c = 0; c < kDpC; c++) m[c] = in[c] ? b[xa + c] : kInf;
-            ys = y0;
+        for (int c = 0; c < C; c++) {
+            const float a = c == 0 ? L : m[c - 1];
+            const float b = m[c];
+            const float cc = c == C - 1 ? R : m[c + 1];
+            const int sa = c == 0 ? sL : s[c - 1];
+            const int sc = c == C - 1 ? sR : s[c + 1];
+            const float best = fminf(fminf(a, b), cc);
+            // leftmost minimum; the off-frame left neighbour of column 0 never
+            // ties (an all-+inf row keeps the chain on the frame, as the
+            // reference's in-frame scan does); on the right an off-frame +inf
+            // can never be strictly smaller
+            const bool isA = (a == best) & (c != 0 || !left_edge), isB = b == best;
+            const int sbc = isB ? s[c] : sc;
+            ns[c] = isA ? sa : sbc;
+            nm[c] = (e[c] + bias[c]) + best;         // e + 0 is e: exact
         }
-        // the band's energies, loaded up front (independent of the recursion)
-        float e[kDpR][kDpC];
 #pragma unroll
-        for (int r = 0; r < kDpR; r++) {
-            const int y = y0 + r;
-#pragma unroll
-            for (int c = 0; c < kDpC; c++)
-                e[r][c] = (y >= ys && y < y1 && in[c]) ? p.map[(long long)y * p.stride + xa + c] : 0.0f;
-        }
-#pragma unroll
-        for (int r = 0; r < kDpR; r++) {
-            const int y = y0 + r;
-            if (y < ys || y >= y1) continue;         // uniform
-            float left = __shfl_up(m[kDpC - 1], 1);
-            float right = __shfl_down(m[0], 1);
-            if (lane == 0) left = kInf;
-            if (lane == kDpLanes - 1) right = kInf;
-            float nm[kDpC];
-            int d[kDpC];
-#pragma unroll
-            for (int c = 0; c < kDpC; c++) {
-                const float a = c == 0 ? left : m[c - 1];
-                const float b = m[c];
-                const float cc = c == kDpC - 1 ? right : m[c + 1];
-                float best = a;                       // leftmost minimum
-                int dd = -1;
-                if (b < best) { best = b; dd = 0; }
-                if (cc < best) { best = cc; dd = 1; }
-                nm[c] = in[c] ? e[r][c] + best : kInf;
-                d[c] = dd;
-            }
-#pragma unroll
-            for (int c = 0; c < kDpC; c++) m[c] = nm[c];
-            int8_t* prow = p.par + (long long)y * w + xa;
-#pragma unroll
-            for (int c = 0; c < kDpC; c++)
-                if (own[c]) prow[c] = (int8_t)d[c];
-        }
-        float* bo = p.bound + (long long)j * w;
-#pragma unroll
-        for (int c = 0; c < kDpC; c++)
-            if (own[c]) bo[xa + c] = m[c];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        if (lane == 0) __hip_atomic_store(&p.flags[k], (unsigned)(j + 1), __ATOMIC_RELEASE,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
+        for (int c = 0; c < C; c++) { m[c] = nm[c]; s[c] = ns[c]; }
+    };
 
-// column where the parent chain from (band j's last row, x) leaves band j:
-// the column in row y0 - 1 (row 0 for band 0)
-__global__ __launch_bounds__(256) void dcte_seam_jump(const DpParams p)
-{
-    const int x = blockIdx.x * 256 + threadIdx.x, j = blockIdx.y;
-    if (x >= p.w || *p.err) return;
-    const int y0 = j * kDpR, y1 = min(p.h, y0 + kDpR);
-    int cur = x;
-    for (int y = y1 - 1; y >= max(y0, 1); y--) cur += p.par[(long long)y * p.w + cur];
-    p.jump[(long long)j * p.w + x] = cur;
+    auto publish = [&](int j) {                      // band j's last row (row 0 for h = 1)
+        if (own) {
+#pragma unroll
+            for (int c = 0; c < C; c++) {
+                const unsigned long long word =
+                    ((unsigned long long)p.epoch << 32) | (unsigned)__float_as_int(m[c]);
+                __hip_atomic_store(p.xch + (long long)j * pw + xa + c, word, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                p.jump[(long long)j * pw + xa + c] = s[c];
+            }
+        }
+    };
+
+    auto take_halo = [&](int j) -> bool {            // band j - 1's last row, halo columns
+        const unsigned long long* xo = p.xch + (long long)(j - 1) * pw;
+        bool need[C];
+#pragma unroll
+        for (int c = 0; c < C; c++) need[c] = in[c] && !own;
+#ifdef DCTE_DP_NOXCH   // timing experiment only: no wait on the neighbours (wrong seams)
+        for (int c = 0; c < C; c++) need[c] = false;
+#endif
+        unsigned spins = 0;
+        for (;;) {
+            unsigned long long v[C];
+#pragma unroll
+            for (int c = 0; c < C; c++)
+                v[c] = __hip_atomic_load(xo + (xoff[c] >> 2), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+            bool ok = true;
+#pragma unroll
+            for (int c = 0; c < C; c++) ok = ok && (!need[c] || (unsigned)(v[c] >> 32) == p.epoch);
+            if (__all(ok)) {
+#pragma unroll
+                for (int c = 0; c < C; c++)
+                    if (need[c]) m[c] = __int_as_float((int)(unsigned)v[c]);
+                return true;
+            }
+            if ((++spins & 255) == 0) {
+                if (spins > kDpSpinLimit) {
+                    __hip_atomic_fetch_or(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    return false;
+                }
+                if (__hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    };
+
+    // row 0 seeds M; bands j = 0 .. nb - 1 cover rows [1 + j kDpR, 1 + (j + 1) kDpR)
+    {
+        float e0[C];
+        set_map(0);
+        load_row(e0, 0);
+#pragma unroll
+        for (int c = 0; c < C; c++) { m[c] = e0[c]; s[c] = xa + c; }
+    }
+    // ring of kDpNB chunks of kDpQ rows: chunk i + kDpNB - 1 is loaded while
+    // chunk i runs.  A band's body is straight-line code, so the compiler
+    // counts outstanding loads exactly (a loop-carried count would degrade
+    // to waiting for everything).
+    constexpr int kCh = kDpR / kDpQ;                 // chunks per band
+    float ring[kDpNB][kDpQ][C];
+#pragma unroll
+    for (int i = 0; i < kDpNB - 1; i++)
+#pragma unroll
+        for (int r = 0; r < kDpQ; r++) load_row(ring[i][r], 1 + i * kDpQ + r);
+    set_map(min(1, h - 1));
+    for (int j = 0; j < p.nb; j++) {
+        const int y0 = 1 + j * kDpR;
+        if (j > 0) {
+            publish(j - 1);
+            if (!take_halo(j)) return;
+#pragma unroll
+            for (int c = 0; c < C; c++) s[c] = xa + c;   // chains enter band j at row y0 - 1
+        }
+        if (y0 + kDpR <= h) {
+#pragma unroll
+            for (int i = 0; i < kCh; i++) {
+#pragma unroll
+                for (int r = 0; r < kDpQ; r++)
+                    load_row(ring[(i + kDpNB - 1) % kDpNB][r], (i + kDpNB - 1) * kDpQ + r);
+#pragma unroll
+                for (int r = 0; r < kDpQ; r++) step(ring[i % kDpNB][r]);
+            }
+        } else {                                     // the last, partial band
+#pragma unroll
+            for (int i = 0; i < kCh; i++) {
+#pragma unroll
+                for (int r = 0; r < kDpQ; r++)
+                    load_row(ring[(i + kDpNB - 1) % kDpNB][r], (i + kDpNB - 1) * kDpQ + r);
+#pragma unroll
+                for (int r = 0; r < kDpQ; r++)
+                    if (y0 + i * kDpQ + r < h) step(ring[i % kDpNB][r]);
+            }
+        }
+        if (y0 + kDpR < h) set_map(y0 + kDpR);       // the ring already holds its first rows
+    }
+    // the last band's row is where the walk starts
+    publish(p.nb - 1);
 }
 
 __global__ __launch_bounds__(256) void dcte_seam_sjump(const DpParams p)
@@ -164,8 +268,8 @@ __global__ __launch_bounds__(256) void dcte_seam_sjump(const DpParams p)
     if (x >= p.w || *p.err) return;
     const int blo = J * kDpG, bhi = min(p.nb, blo + kDpG) - 1;
     int cur = x;
-    for (int b = bhi; b >= blo; b--) cur = p.jump[(long long)b * p.w + cur];
-    p.sjump[(long long)J * p.w + x] = cur;
+    for (int b = bhi; b >= blo; b--) cur = min(max(p.jump[(long long)b * p.pw + cur], 0), p.w - 1);
+    p.sjump[(long long)J * p.pw + x] = cur;
 }
 
 constexpr int kWalkThreads = 1024;
@@ -176,17 +280,26 @@ __global__ __launch_bounds__(kWalkThreads) void dcte_seam_walk(const DpParams p)
     __shared__ int si[kWalkThreads / 64];
     __shared__ int xstar;
     const int tx = threadIdx.x, w = p.w, h = p.h;
+    const long long pw = p.pw;
     if (*p.err) {
         for (int y = tx; y < h; y += kWalkThreads) p.seam[y] = -1;
         return;
     }
     // leftmost minimum of the last row (= the last band's published row)
-    const float* last = p.bound + (long long)(p.nb - 1) * w;
+    const unsigned long long* last = p.xch + (long long)(p.nb - 1) * pw;
     float bv = __builtin_inff();
     int bi = 0x7fffffff;
+    int stale = 0;
     for (int x = tx; x < w; x += kWalkThreads) {
-        const float v = last[x];
+        const unsigned long long word = last[x];
+        const float v = __int_as_float((int)(unsigned)word);
+        stale |= (unsigned)(word >> 32) != p.epoch;  // every column published by this call
         if (v < bv) { bv = v; bi = x; }             // increasing x: strict < keeps the first
+    }
+    if (__syncthreads_or(stale)) {
+        for (int y = tx; y < h; y += kWalkThreads) p.seam[y] = -1;
+        if (tx == 0) *p.err = 2u;                    // dcte_seam_rows stands down
+        return;
     }
     for (int o = 32; o > 0; o >>= 1) {
         const float ov = __shfl_xor(bv, o);
@@ -205,7 +318,7 @@ __global__ __launch_bounds__(kWalkThreads) void dcte_seam_walk(const DpParams p)
         int cur = xstar;
         p.sx[ns - 1] = cur;
         for (int J = ns - 1; J > 0; J--) {
-            cur = p.sjump[(long long)J * w + cur];
+            cur = min(max(p.sjump[(long long)J * pw + cur], 0), w - 1);
             p.sx[J - 1] = cur;
         }
     }
@@ -216,30 +329,113 @@ __global__ __launch_bounds__(kWalkThreads) void dcte_seam_walk(const DpParams p)
         int cur = p.sx[J];
         for (int b = bhi; b >= blo; b--) {
             p.bx[b] = cur;
-            cur = p.jump[(long long)b * w + cur];
+            cur = min(max(p.jump[(long long)b * pw + cur], 0), w - 1);
+        }
+    }
+}
+
+// Rows of each band, one wave per band, all bands at once: the wave re-runs
+// the recursion over its band in a 256-column window centred on bx[b] (the
+// seam's column at the band's last row), from the exact M row above the band
+// (row 0's energies, or band b - 1's published row), keeping every M row in
+// LDS; the chain moves at most one column per row, so every value it reads is
+// exact (the window's garbage edges decay inward one column per row: 128 >>
+// kDpR), and the same floats and rule as dcte_seam_dp give the same parents.
+// Lane 0 then walks the band bottom-up through LDS.
+constexpr int kRwC = 4;                              // columns per lane
+constexpr int kRwSpan = kDpLanes * kRwC;             // 256-column window
+static_assert(kRwSpan / 2 > 2 * kDpR, "the window's exact core holds every chain of a band");
+
+__global__ __launch_bounds__(kDpLanes) void dcte_seam_rows(const DpParams p)
+{
+    __shared__ float ml[kDpR][kRwSpan];              // M rows y0 - 1 .. y0 + kDpR - 2
+    if (*p.err) return;
+    const int b = blockIdx.x, lane = threadIdx.x;
+    const int w = p.w, h = p.h;
+    const int y0 = 1 + b * kDpR, y1 = min(h, y0 + kDpR);   // band b: rows [y0, y1)
+    const int xb = p.bx[b];
+    if (lane == 0) p.seam[max(y1, y0) - 1] = xb;     // h = 1: the one band is empty
+    if (y1 <= y0) return;
+    const float kInf = __builtin_inff();
+    const int xw = xb - kRwSpan / 2;                 // window's first column
+    const int xa = xw + lane * kRwC;
+    long long xc[kRwC];
+    float bias[kRwC], m[kRwC];
+#pragma unroll
+    for (int c = 0; c < kRwC; c++) {
+        const int x = xa + c;
+        xc[c] = min(max(x, 0), w - 1);
+        bias[c] = (x == -1 || x == w) ? kInf : 0.0f;
+    }
+    if (b == 0) {
+#pragma unroll
+        for (int c = 0; c < kRwC; c++) m[c] = p.map[xc[c]];
+    } else {
+        const unsigned long long* xo = p.xch + (long long)(b - 1) * p.pw;
+#pragma unroll
+        for (int c = 0; c < kRwC; c++) m[c] = __int_as_float((int)(unsigned)xo[xc[c]]);
+    }
+#pragma unroll
+    for (int c = 0; c < kRwC; c++) ml[0][lane * kRwC + c] = m[c];
+    for (int y = y0; y < y1 - 1; y++) {              // rows whose M a parent lookup reads
+        float e[kRwC];
+#pragma unroll
+        for (int c = 0; c < kRwC; c++) e[c] = p.map[(long long)y * p.stride + xc[c]];
+        const float L = __int_as_float(wave_shr1(__float_as_int(m[kRwC - 1])));
+        const float R = __int_as_float(wave_shl1(__float_as_int(m[0])));
+        float nm[kRwC];
+#pragma unroll
+        for (int c = 0; c < kRwC; c++) {
+            const float a = c == 0 ? L : m[c - 1];
+            const float cc = c == kRwC - 1 ? R : m[c + 1];
+            nm[c] = (e[c] + bias[c]) + fminf(fminf(a, m[c]), cc);
+        }
+#pragma unroll
+        for (int c = 0; c < kRwC; c++) {
+            m[c] = nm[c];
+            ml[y - y0 + 1][lane * kRwC + c] = m[c];
         }
     }
     __syncthreads();
-    // rows per band
-    for (int b = tx; b < p.nb; b += kWalkThreads) {
-        const int y0 = b * kDpR, y1 = min(h, y0 + kDpR);
-        int cur = p.bx[b];
-        p.seam[y1 - 1] = cur;
-        for (int y = y1 - 1; y > y0; y--) {
-            cur += p.par[(long long)y * w + cur];
-            p.seam[y - 1] = cur;
-        }
+    if (lane != 0) return;
+    // the parent of (y, x) is the leftmost minimum of M[y - 1][x - 1 .. x + 1],
+    // off-frame columns never chosen (as in the DP)
+    int cur = xb;
+    for (int y = y1 - 1; y >= y0; y--) {
+        const float* up = ml[y - y0];                // M row y - 1
+        const int i = cur - xw;
+        const float a = cur > 0 ? up[i - 1] : kInf;
+        const float bb = up[i];
+        const float c = cur < w - 1 ? up[i + 1] : kInf;
+        const float best = fminf(fminf(a, bb), c);
+        cur += (cur > 0 && a == best) ? -1 : (bb == best ? 0 : 1);
+        cur = min(max(cur, 0), w - 1);               // NaN maps only: stay addressable
+        p.seam[y - 1] = cur;
     }
 }
 
 hipError_t launch_seam_find(const DpParams& p, hipStream_t s)
 {
-    if (p.w < 1 || p.h < 1) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(dcte_seam_dp, dim3(p.ntiles), dim3(kDpLanes), 0, s, p);
-    hipLaunchKernelGGL(dcte_seam_jump, dim3((p.w + 255) / 256, p.nb), dim3(256), 0, s, p);
+    if (p.w < 1 || p.h < 1 || p.pw < (long long)p.ntiles * kDpT) return hipErrorInvalidValue;
+    const int per = (p.ntiles + kXcds - 1) / kXcds;
+    hipLaunchKernelGGL(dcte_seam_dp, dim3(per * kXcds), dim3(kDpLanes), 0, s, p);
     hipLaunchKernelGGL(dcte_seam_sjump, dim3((p.w + 255) / 256, p.ns), dim3(256), 0, s, p);
     hipLaunchKernelGGL(dcte_seam_walk, dim3(1), dim3(kWalkThreads), 0, s, p);
+    hipLaunchKernelGGL(dcte_seam_rows, dim3(p.nb), dim3(kDpLanes), 0, s, p);
     return hipGetLastError();
+}
+
+// tiles the DP can run at once (every tile must be resident: tiles wait on
+// their neighbours)
+int dp_max_tiles(int device)
+{
+    int cus = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+        return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dcte_seam_dp, kDpLanes, 0) !=
+        hipSuccess)
+        return 0;
+    return cus * per_cu;
 }
 
 }  // namespace dcte

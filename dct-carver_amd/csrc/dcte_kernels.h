@@ -73,13 +73,14 @@ struct DpParams {
     long long stride;        // floats
     int w, h;
     int nb, ns, ntiles;      // bands (dp_band_rows rows), super-bands, column tiles
-    float* bound;            // nb x w: cumulative energy at each band's last row
-    int8_t* par;             // h x w: parent offset -1 / 0 / +1 (rows >= 1)
-    int* jump;               // nb x w
-    int* sjump;              // ns x w
+    long long pw;            // padded row length of xch / par / jump / sjump (>= ntiles * tile)
+    unsigned epoch;          // tag of this call's hand-off words (never 0)
+    unsigned long long* xch; // nb x pw: {M at the band's last row (f32 bits), epoch << 32}
+    int* jump;               // nb x pw: column where the chain from (band's last row, x)
+                             // leaves the band (row y0 - 1; row 0 for band 0)
+    int* sjump;              // ns x pw
     int* sx;                 // ns
     int* bx;                 // nb
-    unsigned* flags;         // ntiles, zeroed before the launch
     unsigned* err;           // 1, zeroed before the launch
     int* seam;               // h: column removed per row (-1 everywhere on failure)
 };
@@ -93,6 +94,7 @@ hipError_t launch_seam_find(const DpParams& p, hipStream_t s);
 int dp_tile_cols();
 int dp_band_rows();
 int dp_super_bands();
+int dp_max_tiles(int device);
 
 // geometry the launcher uses (exported for tests / bench)
 int map_tile_w(int n);

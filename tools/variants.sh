@@ -8,11 +8,14 @@ HIPCC=/opt/rocm/bin/hipcc
 BASE="-O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -fPIC --offload-arch=gfx950"
 build() {  # name extra-flags...
   local name=$1; shift
-  $HIPCC $BASE "$@" -c -o build/variants/$name.k.o csrc/dcte_kernels.hip
-  $HIPCC $BASE "$@" -c -o build/variants/$name.c.o csrc/dcte_capi.cpp
-  $HIPCC $BASE "$@" -c -o build/variants/$name.n.o csrc/dcte_norm.hip
-  $HIPCC --offload-arch=gfx950 -shared -o build/variants/$name.so build/variants/$name.k.o build/variants/$name.n.o build/variants/$name.c.o
-  rm -f build/variants/$name.k.o build/variants/$name.c.o build/variants/$name.n.o
+  local objs=""
+  for src in csrc/dcte_kernels.hip csrc/dcte_norm.hip csrc/dcte_seam.hip csrc/dcte_dp.hip csrc/dcte_capi.cpp; do
+    local o=build/variants/$name.$(basename $src).o
+    $HIPCC $BASE "$@" -c -o $o $src
+    objs="$objs $o"
+  done
+  $HIPCC --offload-arch=gfx950 -shared -o build/variants/$name.so $objs
+  rm -f $objs
   echo built $name
 }
 while read -r name flags; do
