@@ -124,18 +124,14 @@ void dcte_seam_dp(const DpParams p)
     auto load_row = [&](float (&e)[C], int r) {      // row r of the current map window
 #pragma unroll
         for (int c = 0; c < C; c++)
-#ifndef DCTE_DP_NOLOAD   // timing experiment only: synthetic energies, no map reads
             e[c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                                  ers, (int)xoff[c], r * rowb, 0));
-#else
-            e[c] = (float)((r * 7 + c + lane) & 15);
-#endif
     };
     float m[C];
     int s[C];
     auto step = [&](const float (&e)[C]) {
-        float L = __int_as_float(wave_shr1(__float_as_int(m[C - 1])));
-        float R = __int_as_float(wave_shl1(__float_as_int(m[0])));
+        const float L = __int_as_float(wave_shr1(__float_as_int(m[C - 1])));
+        const float R = __int_as_float(wave_shl1(__float_as_int(m[0])));
         const int sL = wave_shr1(s[C - 1]);
         const int sR = wave_shl1(s[0]);
         float nm[C];
@@ -179,9 +175,6 @@ void dcte_seam_dp(const DpParams p)
         bool need[C];
 #pragma unroll
         for (int c = 0; c < C; c++) need[c] = in[c] && !own;
-#ifdef DCTE_DP_NOXCH   // timing experiment only: no wait on the neighbours (wrong seams)
-        for (int c = 0; c < C; c++) need[c] = false;
-#endif
         unsigned spins = 0;
         for (;;) {
             unsigned long long v[C];

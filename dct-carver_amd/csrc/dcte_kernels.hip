@@ -51,6 +51,12 @@ constexpr int kThreads = 256;
 #ifndef DCTE_MIN_WAVES
 #define DCTE_MIN_WAVES 1   // __launch_bounds__ minimum waves per SIMD
 #endif
+#ifndef DCTE_DB
+#define DCTE_DB 1          // N <= 8: double-buffered LDS staging, one barrier per row group
+#endif
+#ifndef DCTE_XBAL
+#define DCTE_XBAL 1        // halo-column luma conversions spread one per lane of the last wave
+#endif
 constexpr unsigned kBufFlags = 0x00020000u;  // gfx9 raw buffer dword3
 
 // SEM = kSemLqr    : liblqr callback window, offsets -(N/2-1)..N/2
@@ -97,8 +103,12 @@ __global__ __launch_bounds__(kThreads, DCTE_MIN_WAVES) void dcte_map(const MapPa
     constexpr int NDW = Gm::template ndw<BPP>();
     constexpr int DPT = Gm::template dpt<BPP>();         // raw dwords per lane per row
 
-    __shared__ uint32_t raw[G][NDW];
-    __shared__ float lum[G][LWP];
+    // N <= 8: raw / lum double-buffered, so a row group needs one barrier
+    // (N = 16 keeps one buffer: its LDS combine of partial maxima adds one anyway)
+    constexpr bool kDB = DCTE_DB && S == 1;
+    constexpr int NB = kDB ? 2 : 1;
+    __shared__ uint32_t raw[NB][G][NDW];
+    __shared__ float lum[NB][G][LWP];
     // S = 4 (N = 16): per-wave partial maxima of the group's rows; only the
     // waves owning k1 = 0 (q = 0) and k1 = 1 (q = 2) carry an edge candidate
     __shared__ float part_t[S == 4 ? G : 1][S == 4 ? 4 : 1][S == 4 ? 64 : 1];
@@ -184,9 +194,8 @@ __global__ __launch_bounds__(kThreads, DCTE_MIN_WAVES) void dcte_map(const MapPa
             if (k < p.fix_cap) p.fix_list[k] = (unsigned)((y - p.y0) * w + xx);
         }    };
 
-    issue(0);
-    for (int g = 0; g < ngroups; g++) {
-        // stage raw bytes of group g, then prefetch group g + 1
+    // raw dwords of group gg (prefetched in pref) -> raw[b]
+    auto stage = [&](int gg, int b) {
 #pragma unroll
         for (int q = 0; q < DPT; q++) {
             const int dw = tx + q * kThreads;
@@ -195,47 +204,59 @@ __global__ __launch_bounds__(kThreads, DCTE_MIN_WAVES) void dcte_map(const MapPa
                 for (int u = 0; u < G; u++) {
                     uint32_t v = pref[u][q];
                     if (tail_wg) {                 // uniform; a handful of WGs
-                        int i = g * G + u;
+                        int i = gg * G + u;
                         uint32_t a = (row_start(i < n_in ? i : n_in - 1) & ~3u) + 4u * dw;
                         if (a == nrec4) v = tail;
                     }
-                    raw[u][dw] = v;
+                    raw[b][u][dw] = v;
                 }
             }
         }
-        if (g + 1 < ngroups) issue(g + 1);
-        __syncthreads();
-        // bytes -> exact integer luma (biased), one column per lane (+ halo)
-        for (int cc = tx; cc < LW; cc += kThreads) {
-            int xc = clampi(x0 - HL + cc, 0, w - 1);
+    };
+    // bytes -> exact integer luma (biased) of row u of group gg, column cc
+    auto luma_at = [&](int gg, int b, int u, int cc) {
+        const int xc = clampi(x0 - HL + cc, 0, w - 1);
+        const uint32_t off = (row_start(gg * G + u) & 3u) + (uint32_t)((xc - xs) * BPP);
+        const uint8_t* rb = reinterpret_cast<const uint8_t*>(&raw[b][u][0]);
+        uint32_t c0 = rb[off], c1 = 0, c2 = 0;
+        if constexpr (BPP >= 3) {
+            c1 = rb[off + 1];
+            c2 = rb[off + 2];
+        }
+        int L;
+        if constexpr (SEM == kSemLqr) {
+            L = (BPP == 1) ? kLumaGrey * (int)c0
+                           : kLumaR * (int)c0 + kLumaG * (int)c1 + kLumaB * (int)c2;
+            L -= kLumaBias;
+        } else {
+            L = (int)preview_luma(c0, c1, c2, BPP) - kPreviewBias;
+        }
+        lum[b][u][cc] = (float)L;
+    };
+    auto convert = [&](int gg, int b) {
+        constexpr int X = LW - kThreads;                 // halo columns past one per lane
+        if constexpr (DCTE_XBAL && X > 0 && X * G <= 64) {
+            // one column per lane for all G rows; the X * G halo conversions
+            // go one per lane to the last wave instead of G rows to X lanes
+            // of the first (which would hold the whole workgroup at the barrier)
 #pragma unroll
-            for (int u = 0; u < G; u++) {
-                uint32_t rs = row_start(g * G + u);
-                uint32_t off = (rs & 3u) + (uint32_t)((xc - xs) * BPP);
-                const uint8_t* rb = reinterpret_cast<const uint8_t*>(&raw[u][0]);
-                uint32_t c0 = rb[off], c1 = 0, c2 = 0;
-                if constexpr (BPP >= 3) {
-                    c1 = rb[off + 1];
-                    c2 = rb[off + 2];
-                }
-                int L;
-                if constexpr (SEM == kSemLqr) {
-                    L = (BPP == 1) ? kLumaGrey * (int)c0
-                                   : kLumaR * (int)c0 + kLumaG * (int)c1 + kLumaB * (int)c2;
-                    L -= kLumaBias;
-                } else {
-                    L = (int)preview_luma(c0, c1, c2, BPP) - kPreviewBias;
-                }
-                lum[u][cc] = (float)L;
+            for (int u = 0; u < G; u++) luma_at(gg, b, u, tx);
+            const int l = tx - (kThreads - 64);
+            if (l >= 0 && l < X * G) luma_at(gg, b, l / X, kThreads + l % X);
+        } else {
+            for (int cc = tx; cc < LW; cc += kThreads) {
+#pragma unroll
+                for (int u = 0; u < G; u++) luma_at(gg, b, u, cc);
             }
         }
-        __syncthreads();
-        // row pass + column pass for the G rows of this group
+    };
+    // row pass + column pass for the G rows of group g (luma in lum[b])
+    auto compute = [&](int g, int b) {
         static_for<G>([&](auto U) {
             constexpr int u = decltype(U)::value;
             const int i = g * G + u;
             if (i < n_in) {
-                row_pass<N>(&lum[u][0], c, lane_p, ring[u % N]);
+                row_pass<N>(&lum[b][u][0], c, lane_p, ring[u % N]);
                 if (i >= N - 1) {
                     float mt, me;
                     Cols<N>::template run<(u + 1) % N>(ring, lane_p, mt, me);
@@ -261,6 +282,37 @@ __global__ __launch_bounds__(kThreads, DCTE_MIN_WAVES) void dcte_map(const MapPa
                          fmaxf(part_e[u][0][c], part_e[u][1][c]));
                 }
             }
+        }
+    };
+
+    issue(0);
+    if constexpr (kDB) {
+        // One barrier per group: group g is converted and group g + 1 staged
+        // before it, group g's passes run after it.  raw[b] / lum[b] are
+        // rewritten only after every wave has passed the barrier that follows
+        // their last reads (convert(g - 1) / compute(g - 2)).
+        stage(0, 0);
+        if (ngroups > 1) issue(1);
+        __syncthreads();
+        for (int g = 0; g < ngroups; g++) {
+            const int b = g & 1;
+            convert(g, b);
+            if (g + 1 < ngroups) {
+                stage(g + 1, b ^ 1);
+                if (g + 2 < ngroups) issue(g + 2);
+            }
+            __syncthreads();
+            compute(g, b);
+        }
+    } else {
+        for (int g = 0; g < ngroups; g++) {
+            // stage raw bytes of group g, then prefetch group g + 1
+            stage(g, 0);
+            if (g + 1 < ngroups) issue(g + 1);
+            __syncthreads();
+            convert(g, 0);
+            __syncthreads();
+            compute(g, 0);
         }
     }
 }

@@ -123,6 +123,47 @@ DCTE_HD float dct8_k1_max(const float x[8], float m, float& edge)
     return max2in(m, t3 + t1, t0 + t2);
 }
 
+// A k1 >= 1 column with its outputs handed back for folding across columns
+// (Cols<8>): v[0..4] enter m_t as magnitudes -- |a| + |b| for X0/X4 (or
+// a - b = X4 alone when X0 is the edge atom C10, EDGE), X2, X6, X3, X5 --
+// and pq = |P| + |Q| = sqrt2 * max(|X1|, |X7|) goes to a chain of its own,
+// scaled by 1/sqrt2 once per pixel (rounding is monotone, so
+// max_i(pq_i) * R == max_i(pq_i * R) bit for bit).
+template <bool EDGE>
+DCTE_HD void dct8_col_parts(const float x[8], float v[5], float& pq, float& edge)
+{
+    float s0 = x[0] + x[7], d0 = x[0] - x[7];
+    float s1 = x[1] + x[6], d1 = x[1] - x[6];
+    float s2 = x[2] + x[5], d2 = x[2] - x[5];
+    float s3 = x[3] + x[4], d3 = x[3] - x[4];
+    float a = s0 + s3, b = s1 + s2, c = s0 - s3, e = s1 - s2;
+    if constexpr (EDGE) {
+        edge = fabsf(a + b);
+        v[0] = a - b;
+    } else {
+        v[0] = fabsf(a) + fabsf(b);
+    }
+    v[1] = fmaf(c, k8E, e * k8F);
+    v[2] = fmaf(c, k8F, -(e * k8E));
+    float t0 = fmaf(d3, k8B, d0 * k8C);
+    float t3 = fmaf(d0, -k8B, d3 * k8C);
+    float t1 = fmaf(d2, k8A, d1 * k8D);
+    float t2 = fmaf(d1, -k8A, d2 * k8D);
+    pq = fabsf(t1 - t3) + fabsf(t0 - t2);
+    v[3] = t3 + t1;
+    v[4] = t0 + t2;
+}
+
+// ten magnitudes into m: five v_max3 with abs modifiers
+DCTE_HD float fold10(float m, const float a[5], const float b[5])
+{
+    m = max2in(m, a[0], a[1]);
+    m = max2in(m, a[2], a[3]);
+    m = max2in(m, a[4], b[0]);
+    m = max2in(m, b[1], b[2]);
+    return max2in(m, b[3], b[4]);
+}
+
 // k1 = 0 column (inputs: exact integer row sums, |x| <= 5.1e6).  X[0] (the
 // DC, unused) is never formed; X4 = (s0 - s1) + (s3 - s2) avoids the large
 // partial sums a = s0 + s3, b = s1 + s2.  X[1] is the edge atom (0,1).

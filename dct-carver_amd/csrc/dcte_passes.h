@@ -19,6 +19,10 @@
 #define DCTE_HD_MEMBER static inline
 #endif
 
+#ifndef DCTE_PQ2
+#define DCTE_PQ2 1   // N = 8: fold |X1|, |X7| through their own chain (dct8_col_parts)
+#endif
+
 namespace dcte {
 
 template <int N>
@@ -52,6 +56,34 @@ struct Cols<8> {
 #pragma unroll
         for (int j = 0; j < 8; j++) col[j] = ring[(O + j) & 7][0];
         mt = dct8_k0_max(col, 0.0f, e0);
+#if DCTE_PQ2
+        // k1 = 1..7 as parts (dct8_col_parts): two columns' magnitudes per
+        // fold10, the seven pq in a chain of their own, scaled once
+        float va[5], vb[5], pq[7], unused;
+        col_at<O>(ring, 1, col);
+        dct8_col_parts<true>(col, va, pq[0], e1);
+        col_at<O>(ring, 2, col);
+        dct8_col_parts<false>(col, vb, pq[1], unused);
+        mt = fold10(mt, va, vb);
+        col_at<O>(ring, 3, col);
+        dct8_col_parts<false>(col, va, pq[2], unused);
+        col_at<O>(ring, 4, col);
+        dct8_col_parts<false>(col, vb, pq[3], unused);
+        mt = fold10(mt, va, vb);
+        col_at<O>(ring, 5, col);
+        dct8_col_parts<false>(col, va, pq[4], unused);
+        col_at<O>(ring, 6, col);
+        dct8_col_parts<false>(col, vb, pq[5], unused);
+        mt = fold10(mt, va, vb);
+        col_at<O>(ring, 7, col);
+        dct8_col_parts<false>(col, va, pq[6], unused);
+        mt = max2in(max2in(mt, va[0], va[1]), va[2], va[3]);
+        mt = fmaxf(mt, fabsf(va[4]));
+        float q = fmaxf(fmaxf(pq[0], pq[1]), pq[2]);
+        q = fmaxf(fmaxf(q, pq[3]), pq[4]);
+        q = fmaxf(fmaxf(q, pq[5]), pq[6]);
+        mt = fmaxf(mt, q * k8R);
+#else
 #pragma unroll
         for (int j = 0; j < 8; j++) col[j] = ring[(O + j) & 7][1];
         mt = dct8_k1_max(col, mt, e1);
@@ -61,7 +93,15 @@ struct Cols<8> {
             for (int j = 0; j < 8; j++) col[j] = ring[(O + j) & 7][k];
             mt = dct8_tex_max(col, mt);
         }
+#endif
         me = fmaxf(e0, e1);
+    }
+
+    template <int O>
+    DCTE_HD_MEMBER void col_at(const float (&ring)[8][8], int k, float (&col)[8])
+    {
+#pragma unroll
+        for (int j = 0; j < 8; j++) col[j] = ring[(O + j) & 7][k];
     }
 };
 

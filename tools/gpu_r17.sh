@@ -8,7 +8,7 @@ rc=$?; tail -3 "$OUT/pytest_dp.log"; [ $rc -eq 0 ] || exit $rc
 : > "$OUT/dp_var.jsonl"
 timeout -k 10 120 python tools/dp_bench.py --size 16384 --check >> "$OUT/dp_var.jsonl" || exit 1
 timeout -k 10 120 python tools/dp_bench.py --size 4096 --check >> "$OUT/dp_var.jsonl" || exit 1
-for v in c1; do
+for v in nb8 nodpp nosrc pure pure_nosrc; do
   timeout -k 10 120 python tools/dp_bench.py --size 16384 --check --lib dct-carver_amd/build/variants/$v.so >> "$OUT/dp_var.jsonl" || exit 1
 done
 cat "$OUT/dp_var.jsonl"
