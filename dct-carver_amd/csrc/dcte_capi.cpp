@@ -770,6 +770,91 @@ int dcte_seam_find(dcte_ctx* ctx, const float* map, int w, int h, int* seam)
     return DCTE_OK;
 }
 
+int dcte_carve(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride, int n,
+               float edges, float textures, int semantics, int seams, int transposed,
+               uint8_t* out, int* seam_cols)
+{
+    if (!ctx) return DCTE_EINVAL;
+    DCTE_ARG(ctx, px && out && valid_n(n) && valid_sem_bpp(semantics, bpp) && w > 0 && h > 0);
+    DCTE_ARG(ctx, rowstride >= (size_t)w * bpp);
+    const int W = transposed ? h : w, H = transposed ? w : h;   // the frame that is carved
+    DCTE_ARG(ctx, seams >= 0 && seams < W);
+    ctx->last_refined = 0;
+    Device& d = ctx->devs[0];
+    int rc = ensure_stream(ctx, d);
+    if (rc) return rc;
+    hipStream_t s = d.stream;
+    auto align = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    // one allocation: carved frame | its map | seams | (transposed) staging frame
+    const size_t pitch = (size_t)W * bpp;
+    const size_t fbytes = align(pitch * (size_t)H);
+    const size_t mbytes = align(sizeof(float) * (size_t)W * (size_t)H);
+    const size_t sbytes = sizeof(int) * (size_t)H * (size_t)(seams > 0 ? seams : 1);
+    rc = ensure_buf(ctx, (void**)&d.d_in, &d.in_cap,
+                    fbytes + mbytes + align(sbytes) + (transposed ? fbytes : 0));
+    if (rc) return rc;
+    uint8_t* d_px = d.d_in;
+    float* d_map = reinterpret_cast<float*>(d.d_in + fbytes);
+    int* d_seams = reinterpret_cast<int*>(d.d_in + fbytes + mbytes);
+    uint8_t* d_tmp = d.d_in + fbytes + mbytes + align(sbytes);
+    FixScratch* f = nullptr;
+    rc = ensure_fix(ctx, d, s, (size_t)W * (size_t)H, &f);
+    if (rc) return rc;
+    DCTE_HIP(ctx, hipMemsetAsync(f->d_count + 1, 0, sizeof(unsigned), s));
+    const size_t spitch = (size_t)w * bpp;                       // source row
+    if (transposed) {
+        DCTE_HIP(ctx, hipMemcpy2DAsync(d_tmp, spitch, px, rowstride, spitch, h,
+                                       hipMemcpyHostToDevice, s));
+        DCTE_HIP(ctx, dcte::launch_transpose_u8(d_tmp, (long long)spitch, h, w, bpp, d_px,
+                                                (long long)pitch, s));
+    } else {
+        DCTE_HIP(ctx, hipMemcpy2DAsync(d_px, pitch, px, rowstride, pitch, h,
+                                       hipMemcpyHostToDevice, s));
+    }
+    // map, then (seam -> carve in place + energy update) per step, all in HBM
+    rc = run_device(ctx, d, d_px, (long long)pitch, W, H, bpp, 0, H, 0, H, n, edges, textures,
+                    semantics, d_map, W, s);
+    for (int k = 0; rc == DCTE_OK && k < seams; k++) {
+        int* sk = d_seams + (size_t)k * H;
+        rc = dcte_seam_find_device(ctx, 0, d_map, W, W - k, H, sk, s);
+        if (rc == DCTE_OK)
+            rc = dcte_seam_carve_device(ctx, 0, d_px, (long long)pitch, W - k, H, bpp, sk, d_map, W,
+                                        d_px, (long long)pitch, d_map, W, n, edges, textures,
+                                        semantics, s);
+    }
+    if (rc) {
+        drain(ctx, 1);
+        return rc;
+    }
+    const int Wo = W - seams;
+    if (transposed) {   // H x Wo carved frame -> Wo x H = (h - seams) x w
+        DCTE_HIP(ctx, dcte::launch_transpose_u8(d_px, (long long)pitch, H, Wo, bpp, d_tmp,
+                                                (long long)H * bpp, s));
+        DCTE_HIP(ctx, hipMemcpyAsync(out, d_tmp, (size_t)Wo * (size_t)H * bpp,
+                                     hipMemcpyDeviceToHost, s));
+    } else {
+        DCTE_HIP(ctx, hipMemcpy2DAsync(out, (size_t)Wo * bpp, d_px, pitch, (size_t)Wo * bpp, H,
+                                       hipMemcpyDeviceToHost, s));
+    }
+    std::vector<int> own;
+    int* hs = seam_cols;
+    if (seams > 0 && !hs) {
+        own.resize((size_t)seams * H);
+        hs = own.data();
+    }
+    if (seams > 0)
+        DCTE_HIP(ctx, hipMemcpyAsync(hs, d_seams, sizeof(int) * (size_t)seams * H,
+                                     hipMemcpyDeviceToHost, s));
+    rc = sync_bands(ctx, 1);
+    if (rc) return rc;
+    for (int k = 0; k < seams; k++)
+        if (hs[(size_t)k * H] < 0) {
+            ctx->last_error = "seam search timed out waiting for a neighbour tile";
+            return DCTE_EHIP;
+        }
+    return DCTE_OK;
+}
+
 int dcte_energy_map(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride,
                     int n, float edges, float textures, int semantics, int transposed, float* out)
 {

@@ -41,7 +41,8 @@ EXPORTS = ("dcte_abi_version", "dcte_device_count", "dcte_create", "dcte_destroy
            "dcte_energy_map_device", "dcte_last_refined", "dcte_profile_read", "dcte_strerror",
            "dcte_last_error", "dcte_normalize_u8", "dcte_energy_image_u8", "dcte_minmax_device",
            "dcte_normalize_u8_device", "dcte_seam_carve_device", "dcte_energy_points",
-           "dcte_energy_points_device", "dcte_seam_find_device", "dcte_seam_find")
+           "dcte_energy_points_device", "dcte_seam_find_device", "dcte_seam_find",
+           "dcte_carve")
 
 _lib = None
 
@@ -133,6 +134,8 @@ def lib():
     L.dcte_seam_find_device.argtypes = [vp, i, vp, ll, i, i, vp, vp]
     L.dcte_seam_find.restype = i
     L.dcte_seam_find.argtypes = [vp, vp, i, i, vp]
+    L.dcte_carve.restype = i
+    L.dcte_carve.argtypes = [vp, vp, i, i, i, ctypes.c_size_t, i, f, f, i, i, i, vp, vp]
     L.dcte_strerror.restype = ctypes.c_char_p
     L.dcte_strerror.argtypes = [ctypes.c_int]
     L.dcte_last_error.restype = ctypes.c_char_p
@@ -358,6 +361,29 @@ class Context:
         seam = np.empty(h, np.int32)
         self._check(lib().dcte_seam_find(self._h, E.ctypes.data, w, h, seam.ctypes.data))
         return seam
+
+    def carve(self, px, seams, n=8, edges=0.5, textures=0.5, semantics=DCTE_LQR,
+              transposed=False):
+        """Remove `seams` minimum-energy seams from an HxW[xC] uint8 frame
+        (vertical seams; horizontal with transposed=True) -- lqr_carver_resize's
+        loop (src/render.c:377) on the device.  Returns (carved frame, seams),
+        seams[k] = the pixel removed from each line by step k, in that step's frame."""
+        px = np.asarray(px)
+        if px.dtype != np.uint8 or px.ndim not in (2, 3):
+            raise TypeError("px must be an HxW or HxWxC uint8 array")
+        if px.strides[-1] != 1 or (px.ndim == 3 and px.strides[1] != px.shape[2]):
+            px = np.ascontiguousarray(px)
+        h, w = px.shape[:2]
+        bpp = 1 if px.ndim == 2 else px.shape[2]
+        W, H = (h, w) if transposed else (w, h)
+        if not 0 <= seams < W:
+            raise DcteError(DCTE_EINVAL, f"seams must lie in [0, {W})")
+        out = np.empty(((h - seams, w) if transposed else (h, w - seams)) + px.shape[2:], np.uint8)
+        cols = np.empty((seams, H), np.int32)
+        self._check(lib().dcte_carve(self._h, px.ctypes.data, w, h, bpp, _rowstride(px), n, edges,
+                                     textures, semantics, seams, int(bool(transposed)),
+                                     out.ctypes.data, cols.ctypes.data if seams else None))
+        return out, cols
 
     def seam_find_tensor(self, emap, seam, stream=None, device=0):
         """Device version: emap float32 [H, >=W] (row stride emap.stride(0)), seam int32 [H]."""

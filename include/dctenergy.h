@@ -182,6 +182,25 @@ int dcte_seam_find_device(dcte_ctx *ctx, int device, const float *d_map, long lo
                           int w, int h, int *d_seam, void *stream);
 int dcte_seam_find(dcte_ctx *ctx, const float *map, int w, int h, int *seam);
 
+/* ---- carving a whole frame (host buffers) --------------------------------
+ * Removes `seams` minimum-energy seams one at a time -- the loop liblqr runs
+ * in lqr_carver_resize (src/render.c:377) for the reference's carver set-up
+ * (delta_x 1, rigidity 0, the DCT energy re-evaluated around every removed
+ * seam) [liblqr, unverified]: energy map, then (dcte_seam_find_device ->
+ * dcte_seam_carve_device) per seam, all in HBM on the first device; one
+ * upload, one download.
+ *   transposed 0: vertical seams, out is h rows of (w - seams) pixels;
+ *              1: horizontal seams (the frame is carved transposed, as liblqr
+ *              does for vertical resizes), out is (h - seams) rows of w pixels.
+ *              Rows of out are dense (row stride = width * bpp).
+ *   seam_cols  NULL, or seams * L ints (L = h, or w when transposed): entry
+ *              k * L + i = the pixel removed from line i by step k, counted in
+ *              that step's frame.
+ * 0 <= seams < the carved dimension (w, or h when transposed). */
+int dcte_carve(dcte_ctx *ctx, const uint8_t *px, int w, int h, int bpp, size_t rowstride,
+               int n, float edges, float textures, int semantics, int seams, int transposed,
+               uint8_t *out, int *seam_cols);
+
 /* ---- energy image as 8-bit grey ----------------------
  * DCTE_NORM_PREVIEW: normalize_image (src/render.c:81-109, DOUBLE2GUCHAR of
  *   src/render.h:6): ROUND(255*(E-min)/(max-min)) in double, replicated to

@@ -110,3 +110,64 @@ def test_carve_loop_default_mode(ctx):
     for s in seams:
         host = carve(host, s)
     assert np.array_equal(frame, host)
+
+
+# ---- dcte_carve: the whole loop behind one host call ----------------------
+@pytest.mark.parametrize("n", [4, 8])
+def test_host_carve_refined_equals_cpu_reference_loop(ctx, n):
+    """Refine-all mode: every seam and the final frame equal the CPU loop on
+    the reference's arithmetic."""
+    img = load_input("wilber_rgb_74x59.npy")
+    ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, 1.0)
+    try:
+        out, cols = ctx.carve(img, 10, n, 0.3, 0.7)
+    finally:
+        ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, 4e-6)
+    host = img
+    for k in range(10):
+        ref_seam = O.seam_find(O.energy_map(host, n, 0.3, 0.7))
+        assert np.array_equal(cols[k], ref_seam), f"seam {k}"
+        host = carve(host, ref_seam)
+    assert np.array_equal(out, host)
+
+
+def test_host_carve_equals_device_loop(ctx):
+    img = load_input("natural_rgb_97x41.npy")
+    out, cols = ctx.carve(img, 12, 8, 0.5, 0.5)
+    seams, _, frame, _ = _gpu_loop(ctx, img, 8, 0.5, 0.5, 12)
+    assert np.array_equal(out, frame)
+    assert np.array_equal(cols, np.stack(seams))
+
+
+def test_host_carve_transposed(ctx):
+    """Horizontal seams == vertical seams of the transposed frame, transposed back."""
+    img = load_input("natural_rgb_73x59.npy")
+    out, cols = ctx.carve(img, 9, 8, 0.3, 0.7, transposed=True)
+    tr = np.ascontiguousarray(np.swapaxes(img, 0, 1))
+    out_t, cols_t = ctx.carve(tr, 9, 8, 0.3, 0.7)
+    assert out.shape == (59 - 9, 73, 3)
+    assert np.array_equal(out, np.swapaxes(out_t, 0, 1))
+    assert np.array_equal(cols, cols_t)
+
+
+def test_host_carve_edges(ctx):
+    img = load_input("natural_grey_200x120.npy")
+    out, cols = ctx.carve(img, 0, 8)
+    assert np.array_equal(out, img) and cols.shape == (0, img.shape[0])
+    # strided source rows, carved down to one column
+    view = img[:, 3:8]
+    assert view.strides[0] != view.shape[1]
+    out, cols = ctx.carve(view, 4, 8, 0.3, 0.7)
+    assert out.shape == (img.shape[0], 1)
+    host = np.ascontiguousarray(view)
+    for s in cols:
+        host = carve(host, s)
+    assert np.array_equal(out, host)
+    with pytest.raises(dctenergy.DcteError):
+        ctx.carve(view, 5, 8)
+    L = dctenergy.lib()
+    o = np.empty(16, np.uint8)
+    assert L.dcte_carve(ctx._h, view.ctypes.data, 5, 4, 1, 5, 8, 0.5, 0.5, 0, 5, 0,
+                        o.ctypes.data, None) == dctenergy.DCTE_EINVAL
+    assert L.dcte_carve(ctx._h, view.ctypes.data, 5, 4, 1, 5, 6, 0.5, 0.5, 0, 1, 0,
+                        o.ctypes.data, None) == dctenergy.DCTE_EINVAL
