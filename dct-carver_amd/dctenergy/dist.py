@@ -104,3 +104,59 @@ def exchange_halos(buf, band, group=None):
     if not ops:
         return []
     return dist.batch_isend_irecv(ops)
+
+
+def global_minmax(minmax, group=None):
+    """Frame-wide {min, max} from every rank's band {min, max} (a 2-float
+    tensor, e.g. from dcte_minmax_device), in place: ONE all-reduce of
+    [min, -max] with MIN (negation is exact)."""
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return minmax
+    minmax[1:2].neg_()
+    dist.all_reduce(minmax, op=dist.ReduceOp.MIN, group=group)
+    minmax[1:2].neg_()
+    return minmax
+
+
+def energy_image_u8(ctx, band_map, out_u8, mode, channels=1, device=0, group=None):
+    """This rank's rows of the 8-bit energy layer of a row-sharded frame
+    (display_carver_energy, src/render.c:175-202, on a frame split over
+    ranks): band min/max on the device, one all-reduce of 2 floats, then the
+    band normalised with the frame-wide min/max -- the same bytes the single-
+    device dcte_energy_image_u8 writes for those rows.
+    band_map: contiguous float32 CUDA tensor (own rows); out_u8: its
+    uint8 tensor (x channels)."""
+    import torch
+    if not band_map.is_contiguous() or not out_u8.is_contiguous():
+        raise ValueError("band_map and out_u8 must be contiguous")
+    mm = torch.empty(2, dtype=torch.float32, device=band_map.device)
+    stream = torch.cuda.current_stream(band_map.device).cuda_stream
+    ctx.minmax_device(band_map.data_ptr(), band_map.numel(), mm.data_ptr(), stream, device)
+    global_minmax(mm, group)
+    ctx.normalize_u8_device(band_map.data_ptr(), band_map.numel(), mm.data_ptr(),
+                            out_u8.data_ptr(), mode, channels, stream, device)
+    return out_u8
+
+
+def band_rows(H, k, world):
+    """Own rows [Y0, Y1) of rank k for an even split of H rows (make_band's
+    strong split; equal to the weak split when H = world * rows_per_rank)."""
+    return H * k // world, H * (k + 1) // world
+
+
+def gather_bands(part, band, dst=0, group=None):
+    """Every rank's own rows -> the whole frame on rank `dst` (SURVEY §8e(3));
+    None on the other ranks.  Bands are padded to ceil(H / world) rows so one
+    gather moves them (RCCL: one send per rank over its xGMI link)."""
+    import torch
+    import torch.distributed as dist
+    tall = -(-band.H // band.world)
+    pad = part.new_zeros((tall,) + tuple(part.shape[1:]))
+    pad[:band.own] = part
+    bufs = [torch.empty_like(pad) for _ in range(band.world)] if band.rank == dst else None
+    dist.gather(pad, bufs, dst=dst, group=group)
+    if band.rank != dst:
+        return None
+    return torch.cat([bufs[k][:b - a] for k, (a, b) in
+                      enumerate(band_rows(band.H, k, band.world) for k in range(band.world))])

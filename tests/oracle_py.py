@@ -208,11 +208,12 @@ def ref_dct(win):
 
 
 # ------------------------------------------------------- u8 normalisation
-def normalize_preview(E, channels=1):
+def normalize_preview(E, channels=1, minmax=None):
     """normalize_image (src/render.c:81-109) + DOUBLE2GUCHAR (src/render.h:6) +
-    GIMP ROUND ((int)(x + 0.5)), in double; max == min -> 0 (guarded)."""
+    GIMP ROUND ((int)(x + 0.5)), in double; max == min -> 0 (guarded).
+    minmax: the whole frame's (min, max) when E is one band of it."""
     d = np.asarray(E, dtype=np.float32).astype(np.float64)
-    mn, mx = d.min(), d.max()
+    mn, mx = (d.min(), d.max()) if minmax is None else (float(minmax[0]), float(minmax[1]))
     if not mx > mn:
         v = np.zeros(d.shape, np.uint8)
     else:
@@ -220,11 +221,12 @@ def normalize_preview(E, channels=1):
     return np.repeat(v[..., None], channels, -1) if channels > 1 else v
 
 
-def normalize_lqr(E, channels=1):
+def normalize_lqr(E, channels=1, minmax=None):
     """lqr_carver_get_energy_image as documented in include/dctenergy.h
-    [liblqr, unverified]: (E - min)/(max - min) in float, x255, truncated."""
+    [liblqr, unverified]: (E - min)/(max - min) in float, x255, truncated.
+    minmax: the whole frame's (min, max) when E is one band of it."""
     e = np.asarray(E, dtype=np.float32)
-    mn, mx = e.min(), e.max()
+    mn, mx = (e.min(), e.max()) if minmax is None else (np.float32(minmax[0]), np.float32(minmax[1]))
     if not mx > mn:
         v = np.zeros(e.shape, np.uint8)
     else:

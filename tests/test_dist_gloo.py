@@ -54,12 +54,23 @@ def _worker(rank, world, port, n, weak, q):
             win_rows = np.stack([img[i] for i in rows])
             outs.append(O.energy_map(win_rows, n, 0.3, 0.7, y0=r - 1, y1=r)[0])
         part = np.stack(outs)
-        gathered = [None] * world
-        dist.all_gather_object(gathered, part)
+        # frame-wide min/max by one all-reduce, each band's
+        # u8 rows normalised with it; §8e(3): bands gathered to rank 0
+        mm = D.global_minmax(torch.tensor([part.min(), part.max()], dtype=torch.float32))
+        u8 = O.normalize_lqr(part, minmax=mm.numpy())
+        u8p = O.normalize_preview(part, 3, minmax=mm.numpy())
+        whole = D.gather_bands(torch.from_numpy(part), band)
+        whole_u8 = D.gather_bands(torch.from_numpy(u8), band)
+        whole_u8p = D.gather_bands(torch.from_numpy(u8p), band)
         if rank == 0:
             ref = O.energy_map(full.numpy(), n, 0.3, 0.7)
-            q.put((halo_ok, bool(np.array_equal(np.concatenate(gathered), ref))))
+            ok = (np.array_equal(whole.numpy(), ref)
+                  and mm.tolist() == [float(ref.min()), float(ref.max())]
+                  and np.array_equal(whole_u8.numpy(), O.normalize_lqr(ref))
+                  and np.array_equal(whole_u8p.numpy(), O.normalize_preview(ref, 3)))
+            q.put((halo_ok, bool(ok)))
         else:
+            assert whole is None and whole_u8 is None
             q.put((halo_ok, True))
     finally:
         dist.destroy_process_group()

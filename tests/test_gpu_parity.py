@@ -291,3 +291,21 @@ def test_transposed_map(ctx, n):
         got = ctx.energy_map(img, n, 0.15, 0.85, transposed=True, out=out)
         assert np.array_equal(got, ctx.energy_map(tr, n, 0.15, 0.85)), name
         _assert_tol(got, O.energy_map(tr, n, 0.15, 0.85), name)
+
+
+def test_sharded_energy_image_u8_single_rank(ctx):
+    """dist.energy_image_u8 (band min/max -> all-reduce -> normalise) on one
+    rank equals the fused host entry point; the multi-rank reduction and the
+    band gather are covered with gloo in test_dist_gloo.py."""
+    torch = _torch()
+    from dctenergy import dist as D
+    img = load_input("natural_rgb_97x41.npy")
+    frame = torch.from_numpy(img).cuda()
+    E = torch.empty(img.shape[:2], dtype=torch.float32, device="cuda")
+    ctx.energy_map_tensor(frame, E, 8, 0.3, 0.7)
+    for mode, ch in ((dctenergy.DCTE_NORM_LQR, 1), (dctenergy.DCTE_NORM_PREVIEW, 3)):
+        out = torch.empty(img.shape[:2] + ((ch,) if ch > 1 else ()), dtype=torch.uint8,
+                          device="cuda")
+        D.energy_image_u8(ctx, E, out, mode, ch)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), ctx.energy_image_u8(img, 8, 0.3, 0.7, mode, ch))
