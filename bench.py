@@ -34,8 +34,8 @@ VALU_PEAK_LANE_OPS = 256 * 4 * 64 / 2 * 2.4e9
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--n", type=int, default=8)
     ap.add_argument("--size", type=int, default=16384)
     ap.add_argument("--edges", type=float, default=0.3)
