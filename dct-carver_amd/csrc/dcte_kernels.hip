@@ -18,9 +18,10 @@
 //    (bounds-checked buffer resource, no over-read), prefetched one group of
 //    G rows ahead in registers, staged through LDS, converted to the exact
 //    integer luma domain (dcte_luma.h), staged again, and read back as the
-//    N-wide row windows.  Two barriers per group of G rows.
-//  * N = 16 splits the 16 horizontal frequencies of a column over two lanes
-//    (even / odd k1) to keep the ring at 8 x 16 registers per lane.
+//    N-wide row windows.  For N <= 8 both stages are double-buffered: one
+//    barrier per group of G rows.
+//  * N = 16 splits the 16 horizontal frequencies of a column over the four
+//    waves of a workgroup (4 k1 channels each: a 16 x 4 register ring).
 //  * Pixels whose edge/texture decision falls inside the fp32 error band are
 //    appended to a list and recomputed by dcte_fix in fp64, in the
 //    reference's operation order.
@@ -53,6 +54,9 @@ constexpr int kThreads = 256;
 #endif
 #ifndef DCTE_DB
 #define DCTE_DB 1          // N <= 8: double-buffered LDS staging, one barrier per row group
+#endif
+#ifndef DCTE_XCD
+#define DCTE_XCD 1         // XCD-contiguous tile order (neighbouring strips share an L2)
 #endif
 #ifndef DCTE_XBAL
 #define DCTE_XBAL 1        // halo-column luma conversions spread one per lane of the last wave
@@ -117,9 +121,21 @@ __global__ __launch_bounds__(kThreads, DCTE_MIN_WAVES) void dcte_map(const MapPa
     const int tx = threadIdx.x;
     const int lane_p = (S == 4) ? (tx >> 6) : 0;     // N = 16: wave index = k1 class
     const int c = (S == 4) ? (tx & 63) : tx;         // output column within the strip
-    const int x0 = blockIdx.x * TW;
+    // Workgroups are dealt round-robin over the 8 XCDs in dispatch order; the
+    // remap gives each XCD a contiguous run of tiles (strips of a row band in
+    // order), so the N - 1 halo columns two neighbouring strips both read
+    // come from one L2 instead of being fetched twice.
+    int bx = blockIdx.x, by = blockIdx.y;
+    if constexpr (DCTE_XCD) {
+        const int nwg = gridDim.x * gridDim.y, L = blockIdx.x + gridDim.x * blockIdx.y;
+        const int q = nwg / 8, r = nwg % 8, xcd = L % 8;
+        const int T = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
+        bx = T % gridDim.x;
+        by = T / gridDim.x;
+    }
+    const int x0 = bx * TW;
     const int x = x0 + c;
-    const int ys = p.y0 + blockIdx.y * p.tile_h;
+    const int ys = p.y0 + by * p.tile_h;
     const int ye = min(ys + p.tile_h, p.y1);
     const int n_in = (ye - ys) + N - 1;
     const int ngroups = (n_in + G - 1) / G;
