@@ -17,7 +17,7 @@ timeout -k 10 200 python tools/dp_bench.py --size 16384 --check >> "$OUT/seam_lo
 timeout -k 10 200 python tools/dp_bench.py --size 4096 --check >> "$OUT/seam_loop.jsonl" || exit 1
 cat "$OUT/seam_loop.jsonl"
 cd /tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof_trace" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/prof_trace.log" 2>&1 || { echo "trace failed"; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof_trace" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" > "$OUT/prof_trace.json" 2> "$OUT/prof_trace.log" || { echo "trace failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof_loop" -o run -- python3 "$GRAFT_REPO_ROOT/tools/seam_bench.py" --size 16384 --seams 10 --inplace --find > "$OUT/prof_loop.log" 2>&1 || { echo "loop trace failed"; exit 1; }
 for pmc in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_ANY"; do
   tag=$(echo $pmc | tr ' ' '_')
