@@ -58,6 +58,9 @@ constexpr int kThreads = 256;
 #ifndef DCTE_XCD
 #define DCTE_XCD 1         // XCD-contiguous tile order (neighbouring strips share an L2)
 #endif
+#ifndef DCTE_PRIO
+#define DCTE_PRIO 1        // wave priority while staging / converting a group (A/B: -2 %)
+#endif
 #ifndef DCTE_XBAL
 #define DCTE_XBAL 1        // halo-column luma conversions spread one per lane of the last wave
 #endif
@@ -312,12 +315,18 @@ __global__ __launch_bounds__(kThreads, DCTE_MIN_WAVES) void dcte_map(const MapPa
         __syncthreads();
         for (int g = 0; g < ngroups; g++) {
             const int b = g & 1;
+#if DCTE_PRIO
+            __builtin_amdgcn_s_setprio(DCTE_PRIO);
+#endif
             convert(g, b);
             if (g + 1 < ngroups) {
                 stage(g + 1, b ^ 1);
                 if (g + 2 < ngroups) issue(g + 2);
             }
             __syncthreads();
+#if DCTE_PRIO
+            __builtin_amdgcn_s_setprio(0);
+#endif
             compute(g, b);
         }
     } else {
