@@ -59,7 +59,7 @@ constexpr int kThreads = 256;
 #define DCTE_XCD 1         // XCD-contiguous tile order (neighbouring strips share an L2)
 #endif
 #ifndef DCTE_PRIO
-#define DCTE_PRIO 1        // wave priority while staging / converting a group (A/B: -2 %)
+#define DCTE_PRIO 1        // wave priority while staging / converting a group (A/B: -2 % at N = 8 and 16)
 #endif
 #ifndef DCTE_XBAL
 #define DCTE_XBAL 1        // halo-column luma conversions spread one per lane of the last wave
@@ -332,11 +332,17 @@ __global__ __launch_bounds__(kThreads, DCTE_MIN_WAVES) void dcte_map(const MapPa
     } else {
         for (int g = 0; g < ngroups; g++) {
             // stage raw bytes of group g, then prefetch group g + 1
+#if DCTE_PRIO
+            __builtin_amdgcn_s_setprio(DCTE_PRIO);
+#endif
             stage(g, 0);
             if (g + 1 < ngroups) issue(g + 1);
             __syncthreads();
             convert(g, 0);
             __syncthreads();
+#if DCTE_PRIO
+            __builtin_amdgcn_s_setprio(0);
+#endif
             compute(g, 0);
         }
     }
