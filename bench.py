@@ -41,10 +41,13 @@ def parse():
     ap.add_argument("--edges", type=float, default=0.3)
     ap.add_argument("--textures", type=float, default=0.7)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rows", type=int, default=512)
+    ap.add_argument("--cpu-rows", type=int, default=8192)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: stage halos through host memory (rehearsal of the N>1 path "
                          "on a box with fewer GPUs than ranks)")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: one fixed size x size frame split into row bands "
+                         "over the ranks (BASELINE.json configs[3]) instead of size x size per rank")
     ap.add_argument("--check", action="store_true",
                     help="after timing, recompute every band from regenerated rows (no "
                          "exchange) and require bit-equality")
@@ -66,10 +69,11 @@ def cpu_baseline(frame_rows_host, W, n, e, t, sample_rows):
            "kind": "port",
            "sample": f"rows 0..{sample_rows - 1} x {W} cols of the bench frame (N={n}, "
                      f"e={e}, t={t}); oracle/dcte_oracle.c (bit-identical to the reference "
-                     f"transforms), OpenMP over rows, {dt:.2f} s",
+                     f"transforms), OpenMP over rows, {dt:.2f} s wall = {dt * threads:.1f} "
+                     f"thread-s",
            "host_cpus": os.cpu_count()}
     if O.ref_available():
-        rows1 = max(8, sample_rows // 16)
+        rows1 = max(8, sample_rows // 2)
         L = O.luma_plane(img[:rows1 + n])
         sub = np.ascontiguousarray(L)
         t0 = time.perf_counter()
@@ -79,7 +83,7 @@ def cpu_baseline(frame_rows_host, W, n, e, t, sample_rows):
             "value": round(sub.shape[0] * W / d1 / 1e6, 3), "unit": "Mpx/s", "cores": 1,
             "kind": "reference",
             "sample": f"{sub.shape[0]} rows x {W}: the reference's own src/fft2d transforms "
-                      f"(oracle/_ref) in liblqr build order, luma precomputed, serial"}
+                      f"(oracle/_ref) in liblqr build order, luma precomputed, serial, {d1:.2f} s"}
     return res
 
 
@@ -111,8 +115,12 @@ def main():
             dist.init_process_group("gloo")
 
     n, S = args.n, args.size
-    H, W = world * S, S
-    band = D.make_band(H, rank, world, n, rows_per_rank=S)
+    if args.strong:
+        H, W = S, S
+        band = D.make_band(H, rank, world, n)
+    else:
+        H, W = world * S, S
+        band = D.make_band(H, rank, world, n, rows_per_rank=S)
     buf = torch.zeros((band.rows, W, 3), dtype=torch.uint8, device=dev)
     # own rows of the global frame (generated per global row index); halos
     # arrive through the exchange, never regenerated
@@ -229,14 +237,15 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic natural-like RGB (counter-hash noise), generated on device",
             "config": {
-                "workload": f"{S}x{S} RGB per GPU (global {H}x{W} frame, row bands), "
-                            f"N={n}, edges={e}, textures={t}, liblqr-callback semantics",
-                "frame_per_gpu": [S, S], "global_frame": [H, W], "block": n,
+                "workload": (f"{H}x{W} RGB frame split into {world} row band(s)" if args.strong
+                             else f"{S}x{S} RGB per GPU (global {H}x{W} frame, row bands)")
+                            + f", N={n}, edges={e}, textures={t}, liblqr-callback semantics",
+                "frame_per_gpu": [band.own, W], "global_frame": [H, W], "block": n,
                 "parallelism": f"row-band x{world}" + (", RCCL P2P halo exchange overlapped"
                                                         " with interior rows" if world > 1 else ""),
             },

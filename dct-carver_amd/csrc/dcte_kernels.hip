@@ -38,8 +38,10 @@
 
 namespace dcte {
 
-constexpr int kThreads = 256;
 // build-time tuning knobs (tools/variants.sh A/Bs them on the GPU)
+#ifndef DCTE_WG8
+#define DCTE_WG8 256       // threads per workgroup (= strip width) at N = 8 (64: +0.3 % with DCTE_SC, 4x the halo reads)
+#endif
 #ifndef DCTE_TILE_H
 #define DCTE_TILE_H 128
 #endif
@@ -71,11 +73,20 @@ constexpr unsigned kBufFlags = 0x00020000u;  // gfx9 raw buffer dword3
 // SEM = kSemPreview: GTK preview window, offsets -(c-1)..N-c with
 //                    c = (N-1)/2 (src/dct.h:8-9, src/render.c:43-44, 461),
 //                    u8 luma RGB2LUMINANCE (src/render.h:5)
+template <int N>
+struct MapThreads {
+    static constexpr int value = N == 8 ? DCTE_WG8 : 256;
+    // a one-wave workgroup would otherwise be allowed all 512 VGPRs: hold it
+    // to the 4 waves per SIMD the 256-thread build reaches (<= 128 VGPRs)
+    static constexpr int min_waves = value < 256 ? 4 : DCTE_MIN_WAVES;
+};
+
 template <int N, int SEM>
 struct Geo {
+    static constexpr int T = MapThreads<N>::value;       // threads per workgroup
     static constexpr int S = Lanes<N>::S;                // lanes per output column
     static constexpr int CH = Lanes<N>::CH;              // k1 channels per lane
-    static constexpr int TW = kThreads / S;              // output columns per WG
+    static constexpr int TW = T / S;              // output columns per WG
     static constexpr int HL = SEM == kSemLqr ? N / 2 - 1 : (N - 1) / 2 - 1;   // halo left / top
     static constexpr int HR = N - 1 - HL;                                     // halo right / bottom
     static constexpr int LW = TW + N - 1;                // luma columns per row
@@ -84,7 +95,7 @@ struct Geo {
     template <int BPP>
     static constexpr int ndw() { return (LW * BPP + 3) / 4 + 1; }  // dwords per raw row
     template <int BPP>
-    static constexpr int dpt() { return (ndw<BPP>() + kThreads - 1) / kThreads; }  // per lane
+    static constexpr int dpt() { return (ndw<BPP>() + T - 1) / T; }  // per lane
 };
 
 template <int... Is, class F>
@@ -102,9 +113,10 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? l
 
 // ------------------------------------------------------------------ main kernel
 template <int N, int BPP, int SEM>
-__global__ __launch_bounds__(kThreads, DCTE_MIN_WAVES) void dcte_map(const MapParams p)
+__global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) void dcte_map(const MapParams p)
 {
     using Gm = Geo<N, SEM>;
+    constexpr int kThreads = Gm::T;
     constexpr int S = Gm::S, CH = Gm::CH, TW = Gm::TW, HL = Gm::HL;
     constexpr int LW = Gm::LW, LWP = Gm::LWP, G = Gm::G;
     constexpr int NDW = Gm::template ndw<BPP>();
@@ -448,7 +460,7 @@ __global__ __launch_bounds__(64 * kFixWaves) void dcte_fix(const FixParams p)
 }
 
 // ------------------------------------------------------------------ launchers
-int map_tile_w(int n) { return n == 16 ? Geo<16, kSemLqr>::TW : kThreads; }
+int map_tile_w(int n) { return n == 16 ? Geo<16, kSemLqr>::TW : Geo<8, kSemLqr>::TW; }
 int map_default_tile_h(int n) { return n == 16 ? DCTE_TILE_H16 : DCTE_TILE_H; }
 
 template <int N, int BPP, int SEM>
@@ -456,7 +468,7 @@ static hipError_t launch_map_t(const MapParams& p, hipStream_t s)
 {
     constexpr int TW = Geo<N, SEM>::TW;
     dim3 grid((p.w + TW - 1) / TW, (p.y1 - p.y0 + p.tile_h - 1) / p.tile_h);
-    hipLaunchKernelGGL((dcte_map<N, BPP, SEM>), grid, dim3(kThreads), 0, s, p);
+    hipLaunchKernelGGL((dcte_map<N, BPP, SEM>), grid, dim3(Geo<N, SEM>::T), 0, s, p);
     return hipGetLastError();
 }
 
