@@ -203,6 +203,30 @@ DCTE_HD void dct8_col_sc(const float x[8], float& v1, float ye[2], float ya[2], 
     pq = fabsf(fmaf(u3, -k8rBA, u1)) + fabsf(fmaf(u0, k8rBA, -u2));
 }
 
+// k1 = 0 column in scaled form (inputs: exact integer row sums), folded into
+// the four running maxima.  The DC is never formed; X4 = (s0 - s1) + (s3 - s2)
+// as in dct8_k0_max.  X1 (the edge atom C01) = (A / sqrt2)(p + q) and
+// X7 = (A / sqrt2)(p - q) with p, q as in dct8_col_sc; e0 = |p + q| carries
+// the scale A / sqrt2.  25 VALU ops instead of 33.
+DCTE_HD void dct8_k0_sc(const float x[8], float& m1, float& mE, float& mA, float& mQ, float& e0)
+{
+    float s0 = x[0] + x[7], d0 = x[0] - x[7];
+    float s1 = x[1] + x[6], d1 = x[1] - x[6];
+    float s2 = x[2] + x[5], d2 = x[2] - x[5];
+    float s3 = x[3] + x[4], d3 = x[3] - x[4];
+    float c = s0 - s3, e = s1 - s2;
+    m1 = fmaxf(m1, fabsf((s0 - s1) + (s3 - s2)));
+    mE = max2in(mE, fmaf(e, k8rEF, c), fmaf(c, k8rEF, -e));
+    float u0 = fmaf(d0, k8rCB, d3);
+    float u3 = fmaf(d3, k8rCB, -d0);
+    float u1 = fmaf(d1, k8rDA, d2);
+    float u2 = fmaf(d2, k8rDA, -d1);
+    mA = max2in(mA, fmaf(u3, k8rBA, u1), fmaf(u0, k8rBA, u2));
+    float pp = fmaf(u3, -k8rBA, u1), qq = fmaf(u0, k8rBA, -u2);
+    e0 = fabsf(pp + qq);
+    mQ = fmaxf(mQ, fabsf(pp - qq));
+}
+
 // ten magnitudes into m: five v_max3 with abs modifiers
 DCTE_HD float fold10(float m, const float a[5], const float b[5])
 {

@@ -20,7 +20,7 @@
 #endif
 
 #ifndef DCTE_SC
-#define DCTE_SC 2    // N = 8: k1 >= 1 columns in scaled form (dct8_col_sc), four running maxima; 2 = fold per column
+#define DCTE_SC 1    // N = 8: columns in scaled form (dct8_k0_sc, dct8_col_sc), four running maxima
 #endif
 #ifndef DCTE_PQ2
 #define DCTE_PQ2 1   // N = 8: fold |X1|, |X7| through their own chain (dct8_col_parts)
@@ -56,59 +56,33 @@ struct Cols<8> {
     {
         float col[8];
         float e0, e1;
-#pragma unroll
-        for (int j = 0; j < 8; j++) col[j] = ring[(O + j) & 7][0];
-        mt = dct8_k0_max(col, 0.0f, e0);
-#if DCTE_SC == 2
-        // k1 = 1..7 in scaled form, each column folded as soon as it is formed
+#if DCTE_SC
+        // all eight columns in scaled form (dct8_col_sc, dct8_k0_sc), each
+        // folded into the running maxima m1 (scale 1), mE, mA, mQ as soon as
+        // it is formed; k1 = 1 seeds them and k1 = 0 comes last (fewer live
+        // registers than seeding from k1 = 0)
         float v1, ye[2], ya[2], pq, unused;
         col_at<O>(ring, 1, col);
         dct8_col_sc<true>(col, v1, ye, ya, pq, e1);
-        float m1 = fmaxf(mt, fabsf(v1));
-        float mE = fmaxf(fabsf(ye[0]), fabsf(ye[1]));
-        float mA = fmaxf(fabsf(ya[0]), fabsf(ya[1]));
-        float mQ = pq;
+        float m1 = fabsf(v1), mQ = pq;
+        float mE = fmaxf(fabsf(ye[0]), fabsf(ye[1])), mA = fmaxf(fabsf(ya[0]), fabsf(ya[1]));
 #pragma unroll
         for (int k = 2; k < 8; k++) {
             col_at<O>(ring, k, col);
             dct8_col_sc<false>(col, v1, ye, ya, pq, unused);
-            if (k & 1) m1 = fmaxf(m1, v1); else mQ = fmaxf(mQ, pq);
-            if (k & 1) mQ = fmaxf(mQ, pq); else m1 = fmaxf(m1, v1);
+            m1 = fmaxf(m1, v1);
+            mQ = fmaxf(mQ, pq);
             mE = max2in(mE, ye[0], ye[1]);
             mA = max2in(mA, ya[0], ya[1]);
         }
+        col_at<O>(ring, 0, col);
+        dct8_k0_sc(col, m1, mE, mA, mQ, e0);
         mt = max2in(max2in(m1, mQ * k8sPQ, mE * k8sE), mA * k8sA, 0.0f);
-#elif DCTE_SC
-        // k1 = 1..7 in scaled form: running maxima m1 (scale 1, seeded by the
-        // k1 = 0 column), mE, mA, mQ, each scaled once at the end
-        float v1a, v1b, yea[2], yeb[2], yaa[2], yab[2], pqa, pqb, unused;
-        col_at<O>(ring, 1, col);
-        dct8_col_sc<true>(col, v1a, yea, yaa, pqa, e1);
-        col_at<O>(ring, 2, col);
-        dct8_col_sc<false>(col, v1b, yeb, yab, pqb, unused);
-        float m1 = max2in(mt, v1a, v1b);
-        float mE = max2in(fmaxf(fabsf(yea[0]), fabsf(yea[1])), yeb[0], yeb[1]);
-        float mA = max2in(fmaxf(fabsf(yaa[0]), fabsf(yaa[1])), yab[0], yab[1]);
-        float mQ = fmaxf(pqa, pqb);
-#pragma unroll
-        for (int k = 3; k < 8; k += 2) {
-            col_at<O>(ring, k, col);
-            dct8_col_sc<false>(col, v1a, yea, yaa, pqa, unused);
-            if (k + 1 < 8) {
-                col_at<O>(ring, k + 1, col);
-                dct8_col_sc<false>(col, v1b, yeb, yab, pqb, unused);
-                m1 = max2in(m1, v1a, v1b);
-                mE = max2in(max2in(mE, yea[0], yea[1]), yeb[0], yeb[1]);
-                mA = max2in(max2in(mA, yaa[0], yaa[1]), yab[0], yab[1]);
-                mQ = fmaxf(fmaxf(mQ, pqa), pqb);
-            } else {                                // k1 = 7
-                mE = max2in(mE, yea[0], yea[1]);
-                mA = max2in(mA, yaa[0], yaa[1]);
-                mQ = fmaxf(mQ, pqa);
-            }
-        }
-        mt = max2in(max2in(m1, v1a, mE * k8sE), mA * k8sA, mQ * k8sPQ);
-#elif DCTE_PQ2
+        me = fmaxf(e1, e0 * k8sPQ);
+#else
+        col_at<O>(ring, 0, col);
+        mt = dct8_k0_max(col, 0.0f, e0);
+#if DCTE_PQ2
         // k1 = 1..7 as parts (dct8_col_parts): two columns' magnitudes per
         // fold10, the seven pq in a chain of their own, scaled once
         float va[5], vb[5], pq[7], unused;
@@ -147,6 +121,7 @@ struct Cols<8> {
         }
 #endif
         me = fmaxf(e0, e1);
+#endif
     }
 
     template <int O>
