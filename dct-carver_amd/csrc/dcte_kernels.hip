@@ -52,7 +52,7 @@ namespace dcte {
 #define DCTE_G8 8          // rows per staging group for N = 8 (multiple of 8)
 #endif
 #ifndef DCTE_MIN_WAVES
-#define DCTE_MIN_WAVES 1   // __launch_bounds__ minimum waves per SIMD
+#define DCTE_MIN_WAVES 4   // __launch_bounds__ minimum waves per SIMD (<= 128 VGPRs; N = 16 would take 134)
 #endif
 #ifndef DCTE_DB
 #define DCTE_DB 1          // N <= 8: double-buffered LDS staging, one barrier per row group
@@ -76,9 +76,9 @@ constexpr unsigned kBufFlags = 0x00020000u;  // gfx9 raw buffer dword3
 template <int N>
 struct MapThreads {
     static constexpr int value = N == 8 ? DCTE_WG8 : 256;
-    // a one-wave workgroup would otherwise be allowed all 512 VGPRs: hold it
-    // to the 4 waves per SIMD the 256-thread build reaches (<= 128 VGPRs)
-    static constexpr int min_waves = value < 256 ? 4 : DCTE_MIN_WAVES;
+    // 4 waves per SIMD: <= 128 VGPRs (N = 8 needs 113; N = 16 would take 134
+    // and drop to 3 waves: A/B -2 % with the cap)
+    static constexpr int min_waves = DCTE_MIN_WAVES;
 };
 
 template <int N, int SEM>

@@ -227,6 +227,32 @@ DCTE_HD void dct8_k0_sc(const float x[8], float& m1, float& mE, float& mA, float
     mQ = fmaxf(mQ, fabsf(pp - qq));
 }
 
+// Full 8-point transform for the first (row) pass with the odd half in the
+// scaled form of dct8_col_sc, then materialised: 14 ops instead of 16.  X3
+// comes out negated (-X3); the second pass only takes magnitudes of linear
+// combinations within one channel, so a channel's sign never matters.
+DCTE_HD void dct8_row(const float x[8], float X[8])
+{
+    float s0 = x[0] + x[7], d0 = x[0] - x[7];
+    float s1 = x[1] + x[6], d1 = x[1] - x[6];
+    float s2 = x[2] + x[5], d2 = x[2] - x[5];
+    float s3 = x[3] + x[4], d3 = x[3] - x[4];
+    float a = s0 + s3, b = s1 + s2, c = s0 - s3, e = s1 - s2;
+    X[0] = a + b;
+    X[4] = a - b;
+    X[2] = fmaf(c, k8E, e * k8F);
+    X[6] = fmaf(c, k8F, -(e * k8E));
+    float u0 = fmaf(d0, k8rCB, d3);
+    float u3 = fmaf(d3, k8rCB, -d0);
+    float u1 = fmaf(d1, k8rDA, d2);
+    float u2 = fmaf(d2, k8rDA, -d1);
+    float pp = fmaf(u3, -k8rBA, u1), qq = fmaf(u0, k8rBA, -u2);
+    X[3] = fmaf(u3, k8rBA, u1) * k8sA;
+    X[5] = fmaf(u0, k8rBA, u2) * k8sA;
+    X[1] = (pp + qq) * k8sPQ;
+    X[7] = (pp - qq) * k8sPQ;
+}
+
 // ten magnitudes into m: five v_max3 with abs modifiers
 DCTE_HD float fold10(float m, const float a[5], const float b[5])
 {
@@ -377,6 +403,28 @@ DCTE_HD void dct16(const float x[16], float X[16])
 }
 
 // max over the 16 outputs of an all-texture column, folded into m
+// dct16_tex_max with the even half (the 8-point transform of s, same hat
+// units) in the scaled form of dct8_col_sc: its magnitudes go to the running
+// maxima m (scale 1, which also takes the odd half), mE, mA, mQ.
+DCTE_HD void dct16_tex_sc(const float x[16], float& m, float& mE, float& mA, float& mQ)
+{
+    float s[8], d[8], X[16];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        s[j] = x[j] + x[15 - j];
+        d[j] = x[j] - x[15 - j];
+    }
+    float v1, ye[2], ya[2], pq, unused;
+    dct8_col_sc<false>(s, v1, ye, ya, pq, unused);
+    mE = max2in(mE, ye[0], ye[1]);
+    mA = max2in(mA, ya[0], ya[1]);
+    mQ = fmaxf(mQ, pq);
+    m = fmaxf(m, v1);
+    dct16_odd_fast(d, X);
+#pragma unroll
+    for (int q = 1; q < 16; q += 4) m = fmaxf(fmaxf(m, fabsf(X[q])), fabsf(X[q + 2]));
+}
+
 DCTE_HD float dct16_tex_max(const float x[16], float m)
 {
     float s[8], d[8], X[16];

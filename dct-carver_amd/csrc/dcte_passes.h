@@ -22,6 +22,12 @@
 #ifndef DCTE_SC
 #define DCTE_SC 1    // N = 8: columns in scaled form (dct8_k0_sc, dct8_col_sc), four running maxima
 #endif
+#ifndef DCTE_ROWSC
+#define DCTE_ROWSC 1 // N = 8: odd half of the row pass in scaled form, materialised (dct8_row)
+#endif
+#ifndef DCTE_SC16
+#define DCTE_SC16 1  // N = 16: even halves of the texture columns in scaled form (dct16_tex_sc)
+#endif
 #ifndef DCTE_PQ2
 #define DCTE_PQ2 1   // N = 8: fold |X1|, |X7| through their own chain (dct8_col_parts)
 #endif
@@ -165,6 +171,9 @@ struct Cols<16> {
         float col[16], X[16];
         mt = 0.0f;
         me = 0.0f;
+#if DCTE_SC16
+        float mE = 0.0f, mA = 0.0f, mQ = 0.0f;       // scaled running maxima (dct16_tex_sc)
+#endif
         // channel 0: k1 = 4q' ... special roles for k1 = 0 (q = 0) and k1 = 1 (q = 2)
 #pragma unroll
         for (int j = 0; j < 16; j++) col[j] = ring[(O + j) & 15][0];
@@ -185,14 +194,25 @@ struct Cols<16> {
             for (int k = 1; k < 15; k += 2) mt = fmaxf(fmaxf(mt, fabsf(X[k])), fabsf(X[k + 1]));
             mt = fmaxf(mt, fabsf(X[15]));
         } else {
+#if DCTE_SC16
+            dct16_tex_sc(col, mt, mE, mA, mQ);
+#else
             mt = dct16_tex_max(col, mt);
+#endif
         }
 #pragma unroll
         for (int c = 1; c < 4; c++) {
 #pragma unroll
             for (int j = 0; j < 16; j++) col[j] = ring[(O + j) & 15][c];
+#if DCTE_SC16
+            dct16_tex_sc(col, mt, mE, mA, mQ);
+#else
             mt = dct16_tex_max(col, mt);
+#endif
         }
+#if DCTE_SC16
+        mt = max2in(max2in(mt, mQ * k8sPQ, mE * k8sE), mA * k8sA, 0.0f);
+#endif
     }
 };
 
@@ -204,7 +224,11 @@ DCTE_HD void row_pass(const float* lrow, int c, int p, float (&dst)[Lanes<N>::CH
         float x[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) x[j] = lrow[c + j];
+#if DCTE_SC && DCTE_ROWSC
+        dct8_row(x, dst);
+#else
         dct8(x, dst);
+#endif
     } else if constexpr (N == 4) {
         float x[4];
 #pragma unroll
