@@ -65,7 +65,18 @@ DCTE_HD void dct8_odd(float d0, float d1, float d2, float d3,
 // four outputs instead of 16, and three values to fold instead of four.
 constexpr float k8R = 0.7071067811865475f;  // 1/sqrt2
 
-// full 8-point transform (first pass, and k1 >= 1 columns of the second)
+// scaled-form constants (see dct8_col_sc)
+constexpr float k8rEF = 0.41421356237309503f;  // F / E = tan(pi/8)
+constexpr float k8rCB = 0.66817863791929891f;  // C / B = tan(3 pi/16)
+constexpr float k8rDA = 0.19891236737965800f;  // D / A = tan(pi/16)
+constexpr float k8rBA = 0.84775906502257351f;  // B / A = cos(3 pi/16) / cos(pi/16)
+constexpr float k8sA = 1.3870398453221475f;    // A (scale of the ya chain)
+constexpr float k8sE = 1.3065629648763766f;    // E (scale of the ye chain)
+constexpr float k8sPQ = 0.98078528040323043f;  // A / sqrt2 = cos(pi/16) (scale of the pq chain)
+
+// full 8-point transform (row pass of N = 8; inside the N = 16 transforms).
+// The odd half goes through the scaled form of dct8_col_sc and is then
+// materialised: 14 VALU ops instead of the 16 of dct8_odd.
 DCTE_HD void dct8(const float x[8], float X[8])
 {
     float s0 = x[0] + x[7], d0 = x[0] - x[7];
@@ -77,7 +88,15 @@ DCTE_HD void dct8(const float x[8], float X[8])
     X[4] = a - b;
     X[2] = fmaf(c, k8E, e * k8F);
     X[6] = fmaf(c, k8F, -(e * k8E));
-    dct8_odd(d0, d1, d2, d3, X[1], X[3], X[5], X[7]);
+    float u0 = fmaf(d0, k8rCB, d3);
+    float u3 = fmaf(d3, k8rCB, -d0);
+    float u1 = fmaf(d1, k8rDA, d2);
+    float u2 = fmaf(d2, k8rDA, -d1);
+    float pp = fmaf(u3, -k8rBA, u1), qq = fmaf(u0, k8rBA, -u2);
+    X[1] = (pp + qq) * k8sPQ;
+    X[3] = fmaf(u3, k8rBA, u1) * -k8sA;
+    X[5] = fmaf(u0, k8rBA, u2) * k8sA;
+    X[7] = (pp - qq) * k8sPQ;
 }
 
 // max over |X[0..7]| of a column whose 8 outputs are all texture atoms,
@@ -169,14 +188,6 @@ DCTE_HD void dct8_col_parts(const float x[8], float v[5], float& pq, float& edge
 //   v1 -> scale 1 (|a| + |b| for X0/X4, or a - b = X4 alone when X0 is the
 //         edge atom C10, EDGE);  ye[2] -> scale E;  ya[2] -> scale A;
 //   pq -> scale A / sqrt2.
-constexpr float k8rEF = 0.41421356237309503f;  // F / E = tan(pi/8)
-constexpr float k8rCB = 0.66817863791929891f;  // C / B = tan(3 pi/16)
-constexpr float k8rDA = 0.19891236737965800f;  // D / A = tan(pi/16)
-constexpr float k8rBA = 0.84775906502257351f;  // B / A = cos(3 pi/16) / cos(pi/16)
-constexpr float k8sA = 1.3870398453221475f;    // A (scale of the ya chain)
-constexpr float k8sE = 1.3065629648763766f;    // E (scale of the ye chain)
-constexpr float k8sPQ = 0.98078528040323043f;  // A / sqrt2 = cos(pi/16) (scale of the pq chain)
-
 template <bool EDGE>
 DCTE_HD void dct8_col_sc(const float x[8], float& v1, float ye[2], float ya[2], float& pq,
                          float& edge)
@@ -225,32 +236,6 @@ DCTE_HD void dct8_k0_sc(const float x[8], float& m1, float& mE, float& mA, float
     float pp = fmaf(u3, -k8rBA, u1), qq = fmaf(u0, k8rBA, -u2);
     e0 = fabsf(pp + qq);
     mQ = fmaxf(mQ, fabsf(pp - qq));
-}
-
-// Full 8-point transform for the first (row) pass with the odd half in the
-// scaled form of dct8_col_sc, then materialised: 14 ops instead of 16.  X3
-// comes out negated (-X3); the second pass only takes magnitudes of linear
-// combinations within one channel, so a channel's sign never matters.
-DCTE_HD void dct8_row(const float x[8], float X[8])
-{
-    float s0 = x[0] + x[7], d0 = x[0] - x[7];
-    float s1 = x[1] + x[6], d1 = x[1] - x[6];
-    float s2 = x[2] + x[5], d2 = x[2] - x[5];
-    float s3 = x[3] + x[4], d3 = x[3] - x[4];
-    float a = s0 + s3, b = s1 + s2, c = s0 - s3, e = s1 - s2;
-    X[0] = a + b;
-    X[4] = a - b;
-    X[2] = fmaf(c, k8E, e * k8F);
-    X[6] = fmaf(c, k8F, -(e * k8E));
-    float u0 = fmaf(d0, k8rCB, d3);
-    float u3 = fmaf(d3, k8rCB, -d0);
-    float u1 = fmaf(d1, k8rDA, d2);
-    float u2 = fmaf(d2, k8rDA, -d1);
-    float pp = fmaf(u3, -k8rBA, u1), qq = fmaf(u0, k8rBA, -u2);
-    X[3] = fmaf(u3, k8rBA, u1) * k8sA;
-    X[5] = fmaf(u0, k8rBA, u2) * k8sA;
-    X[1] = (pp + qq) * k8sPQ;
-    X[7] = (pp - qq) * k8sPQ;
 }
 
 // ten magnitudes into m: five v_max3 with abs modifiers

@@ -22,9 +22,6 @@
 #ifndef DCTE_SC
 #define DCTE_SC 1    // N = 8: columns in scaled form (dct8_k0_sc, dct8_col_sc), four running maxima
 #endif
-#ifndef DCTE_ROWSC
-#define DCTE_ROWSC 1 // N = 8: odd half of the row pass in scaled form, materialised (dct8_row)
-#endif
 #ifndef DCTE_SC16
 #define DCTE_SC16 1  // N = 16: even halves of the texture columns in scaled form (dct16_tex_sc)
 #endif
@@ -224,11 +221,7 @@ DCTE_HD void row_pass(const float* lrow, int c, int p, float (&dst)[Lanes<N>::CH
         float x[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) x[j] = lrow[c + j];
-#if DCTE_SC && DCTE_ROWSC
-        dct8_row(x, dst);
-#else
         dct8(x, dst);
-#endif
     } else if constexpr (N == 4) {
         float x[4];
 #pragma unroll
