@@ -102,3 +102,15 @@ def test_band_geometry():
     assert (b0.top, b0.bot, b0.interior(), b0.edges()) == (0, 0, (0, 100), [])
     with pytest.raises(ValueError):
         D.make_band(12, 1, 4, 16)
+
+
+def test_band_geometry_strong_bench():
+    """bench.py --strong: one 16384^2 frame over 1/2/4/8 ranks (configs[3])."""
+    from dctenergy import dist as D
+    for world in (1, 2, 4, 8):
+        bands = [D.make_band(16384, k, world, 8) for k in range(world)]
+        assert [b.own for b in bands] == [16384 // world] * world
+        assert bands[0].Y0 == 0 and bands[-1].Y1 == 16384
+        assert all(a.Y1 == b.Y0 for a, b in zip(bands, bands[1:]))
+        for b in bands:
+            assert b.top == (3 if b.Y0 > 0 else 0) and b.bot == (4 if b.Y1 < 16384 else 0)
