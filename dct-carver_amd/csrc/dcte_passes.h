@@ -169,7 +169,7 @@ struct Cols<16> {
         mt = 0.0f;
         me = 0.0f;
 #if DCTE_SC16
-        float mE = 0.0f, mA = 0.0f, mQ = 0.0f;       // scaled running maxima (dct16_tex_sc)
+        float mE = 0.0f, mA = 0.0f, mQ = 0.0f, m2 = 0.0f;   // scaled running maxima (dct16_tex_sc)
 #endif
         // channel 0: k1 = 4q' ... special roles for k1 = 0 (q = 0) and k1 = 1 (q = 2)
 #pragma unroll
@@ -192,7 +192,7 @@ struct Cols<16> {
             mt = fmaxf(mt, fabsf(X[15]));
         } else {
 #if DCTE_SC16
-            dct16_tex_sc(col, mt, mE, mA, mQ);
+            dct16_tex_sc(col, mt, mE, mA, mQ, m2);
 #else
             mt = dct16_tex_max(col, mt);
 #endif
@@ -202,13 +202,13 @@ struct Cols<16> {
 #pragma unroll
             for (int j = 0; j < 16; j++) col[j] = ring[(O + j) & 15][c];
 #if DCTE_SC16
-            dct16_tex_sc(col, mt, mE, mA, mQ);
+            dct16_tex_sc(col, mt, mE, mA, mQ, m2);
 #else
             mt = dct16_tex_max(col, mt);
 #endif
         }
 #if DCTE_SC16
-        mt = max2in(max2in(mt, mQ * k8sPQ, mE * k8sE), mA * k8sA, 0.0f);
+        mt = max2in(max2in(mt, mQ * k8sPQ, mE * k8sE), mA * k8sA, m2 * k16s2c);
 #endif
     }
 };
