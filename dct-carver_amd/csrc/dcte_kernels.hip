@@ -57,6 +57,9 @@ namespace dcte {
 #ifndef DCTE_DB
 #define DCTE_DB 1          // N <= 8: double-buffered LDS staging, one barrier per row group
 #endif
+#ifndef DCTE_MIN_WAVES16
+#define DCTE_MIN_WAVES16 4 // the same for N = 16
+#endif
 #ifndef DCTE_XCD
 #define DCTE_XCD 1         // XCD-contiguous tile order (neighbouring strips share an L2)
 #endif
@@ -78,7 +81,7 @@ struct MapThreads {
     static constexpr int value = N == 8 ? DCTE_WG8 : 256;
     // 4 waves per SIMD: <= 128 VGPRs (N = 8 needs 113; N = 16 would take 134
     // and drop to 3 waves: A/B -2 % with the cap)
-    static constexpr int min_waves = DCTE_MIN_WAVES;
+    static constexpr int min_waves = N == 16 ? DCTE_MIN_WAVES16 : DCTE_MIN_WAVES;
 };
 
 template <int N, int SEM>

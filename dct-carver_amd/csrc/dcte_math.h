@@ -412,7 +412,8 @@ constexpr float k16c3 = 0.29028467725446233f;   // cos(13 pi/32)
 constexpr float k16s3 = 0.95694033573220894f;   // sin(13 pi/32)
 constexpr float k16s2c = 1.4142135623730951f;   // sqrt2 (scale of the m2 chain)
 
-DCTE_HD void dct16_odd_sc(const float d[8], float& m, float& mE, float& m2)
+template <bool EDGE = false>
+DCTE_HD void dct16_odd_sc(const float d[8], float& m, float& mE, float& m2, float* edge = nullptr)
 {
     // u_n = (a + i b)(cos - i sin) = (a cos + b sin) + i (b cos - a sin)
     float r0 = fmaf(d[7], k16s0, d[0] * k16c0), i0 = fmaf(d[0], -k16s0, d[7] * k16c0);
@@ -422,7 +423,12 @@ DCTE_HD void dct16_odd_sc(const float d[8], float& m, float& mE, float& m2)
     float sr = r0 + r2, si = i0 + i2, tr = r1 + r3, ti = i1 + i3;
     float dr = r0 - r2, di = i0 - i2, er = r1 - r3, ei = i1 - i3;
     // U0 = (s + t), U2 = (s - t), U1 = (dr + ei) + i (di - er), U3 = (dr - ei) + i (di + er)
-    m2 = max2in(m2, sr + tr, si + ti);
+    if constexpr (EDGE) {                       // X1 = sqrt2 Re U0 is the edge atom C01
+        *edge = fabsf(sr + tr);
+        m2 = fmaxf(m2, fabsf(si + ti));
+    } else {
+        m2 = max2in(m2, sr + tr, si + ti);
+    }
     m = fmaxf(m, fabsf(sr - tr) + fabsf(si - ti));
     float u1r = dr + ei, u1i = di - er, u3r = dr - ei, u3i = di + er;
     mE = max2in(mE, fmaf(u1i, k8rEF, u1r), fmaf(u1r, k8rEF, -u1i));
@@ -449,7 +455,7 @@ DCTE_HD void dct16_tex_sc(const float x[16], float& m, float& mE, float& mA, flo
     mQ = fmaxf(mQ, pq);
     m = fmaxf(m, v1);
 #if DCTE_ODD16SC
-    dct16_odd_sc(d, m, mE, m2);
+    dct16_odd_sc<false>(d, m, mE, m2);
 #else
     dct16_odd_fast(d, X);
 #pragma unroll

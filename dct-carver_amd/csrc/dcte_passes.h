@@ -174,6 +174,41 @@ struct Cols<16> {
         // channel 0: k1 = 4q' ... special roles for k1 = 0 (q = 0) and k1 = 1 (q = 2)
 #pragma unroll
         for (int j = 0; j < 16; j++) col[j] = ring[(O + j) & 15][0];
+#if DCTE_SC16 && DCTE_ODD16SC
+        if (q == 0 || q == 2) {
+            // the two edge columns in the scaled forms as well: q = 0 holds
+            // k1 = 0 (exact integer row sums, centred on one of its own
+            // samples so no large partial sum forms; the DC is excluded, X1 =
+            // C01 is the odd half's sqrt2 Re U0), q = 2 holds k1 = 1 (X0 = C10
+            // is the even half's a + b)
+            if (q == 0) {
+                const float ref = col[7];
+#pragma unroll
+                for (int j = 0; j < 16; j++) col[j] -= ref;
+            }
+            float s[8], d[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                s[j] = col[j] + col[15 - j];
+                d[j] = col[j] - col[15 - j];
+            }
+            float v1, ye[2], ya[2], pq, e_even, e_odd;
+            dct8_col_sc<true>(s, v1, ye, ya, pq, e_even);
+            mt = fabsf(v1);
+            mE = max2in(mE, ye[0], ye[1]);
+            mA = max2in(mA, ya[0], ya[1]);
+            mQ = pq;
+            if (q == 0) {
+                dct16_odd_sc<true>(d, mt, mE, m2, &e_odd);
+                me = e_odd * k16s2c;
+            } else {
+                dct16_odd_sc<false>(d, mt, mE, m2);
+                me = e_even;
+            }
+        } else {
+            dct16_tex_sc(col, mt, mE, mA, mQ, m2);
+        }
+#else
         if (q == 0) {
             // exact integer row sums: centre on one of its own samples (exact)
             // so no large partial sum forms; X0 is the DC (excluded), X1 = C01
@@ -197,6 +232,7 @@ struct Cols<16> {
             mt = dct16_tex_max(col, mt);
 #endif
         }
+#endif
 #pragma unroll
         for (int c = 1; c < 4; c++) {
 #pragma unroll
