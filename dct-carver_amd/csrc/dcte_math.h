@@ -278,6 +278,7 @@ DCTE_HD float dct8_k0_max(const float x[8], float m, float& edge)
 constexpr float k4H = 0.7071067811865476f;
 constexpr float k4A = 0.9238795325112867f;
 constexpr float k4B = 0.38268343236508984f;
+constexpr float k4rBA = 0.41421356237309503f;  // k4B / k4A = tan(pi/8)
 
 DCTE_HD void dct4(const float x[4], float X[4])
 {

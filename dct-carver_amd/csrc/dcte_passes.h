@@ -22,6 +22,9 @@
 #ifndef DCTE_SC
 #define DCTE_SC 1    // N = 8: columns in scaled form (dct8_k0_sc, dct8_col_sc), four running maxima
 #endif
+#ifndef DCTE_SC4
+#define DCTE_SC4 1   // N = 4: second pass in scaled form (Cols<4>)
+#endif
 #ifndef DCTE_SC16
 #define DCTE_SC16 1  // N = 16: even halves of the texture columns in scaled form (dct16_tex_sc)
 #endif
@@ -157,7 +160,41 @@ struct ColsSmall {
         }
     }
 };
+#if DCTE_SC4
+// N = 4 in scaled form: X2 = H (s0 - s1) and the rotation X1 = A (d0 + r d1),
+// X3 = A (r d0 - d1), r = B / A, feed running maxima scaled once per pixel
+// (8 VALU ops per column instead of 11).  Edge atoms: X1 of k1 = 0 (scale A)
+// and X0 of k1 = 1 (scale 1).
+template <>
+struct Cols<4> {
+    template <int O>
+    DCTE_HD_MEMBER void run(const float (&ring)[4][4], int, float& mt, float& me)
+    {
+        float m1 = 0.0f, mH = 0.0f, mA = 0.0f, e0 = 0.0f, e1 = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            float c[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) c[j] = ring[(O + j) & 3][k];
+            const float s0 = c[0] + c[3], d0 = c[0] - c[3];
+            const float s1 = c[1] + c[2], d1 = c[1] - c[2];
+            mH = fmaxf(mH, fabsf(s0 - s1));
+            const float x1 = fmaf(d1, k4rBA, d0), x3 = fmaf(d0, k4rBA, -d1);
+            if (k == 0) {
+                e0 = fabsf(x1);
+                mA = fabsf(x3);
+            } else {
+                mA = max2in(mA, x1, x3);
+                if (k == 1) e1 = fabsf(s0 + s1); else m1 = fmaxf(m1, fabsf(s0 + s1));
+            }
+        }
+        mt = max2in(m1, mH * k4H, mA * k4A);
+        me = fmaxf(e1, e0 * k4A);
+    }
+};
+#else
 template <> struct Cols<4> : ColsSmall<4> {};
+#endif
 template <> struct Cols<2> : ColsSmall<2> {};
 
 template <>
