@@ -61,9 +61,15 @@ namespace dcte {
 constexpr int kDpLanes = 64;
 constexpr int kDpC = DCTE_DP_C;                      // columns per lane (1, 2 or 4)
 constexpr int kDpSpan = kDpLanes * kDpC;
-constexpr int kDpR = 16 * kDpC;                      // rows per band (= halo)
+#ifndef DCTE_DP_R
+#define DCTE_DP_R (16 * DCTE_DP_C)
+#endif
+#ifndef DCTE_DP_Q
+#define DCTE_DP_Q 4
+#endif
+constexpr int kDpR = DCTE_DP_R;                      // rows per band (= halo)
 constexpr int kDpT = kDpSpan - 2 * kDpR;             // owned columns per wave
-constexpr int kDpQ = 4;                              // rows per chunk
+constexpr int kDpQ = DCTE_DP_Q;                      // rows per chunk
 #ifndef DCTE_DP_NB
 #define DCTE_DP_NB 4
 #endif
@@ -75,6 +81,7 @@ static_assert(kDpC == 1 || kDpC == 2 || kDpC == 4, "C in {1, 2, 4}");
 static_assert(kDpR % kDpQ == 0 && (kDpR / kDpQ) % kDpNB == 0,
               "a band is a whole number of chunks and of ring turns (static ring slots)");
 static_assert(kDpT >= kDpR, "a halo lies inside one neighbour tile");
+static_assert(kDpR % kDpC == 0, "the halo is a whole number of lanes");
 
 int dp_tile_cols() { return kDpT; }
 int dp_band_rows() { return kDpR; }
