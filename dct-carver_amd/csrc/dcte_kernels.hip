@@ -216,9 +216,10 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
     // decision + store (+ refinement flag) of output pixel (x, y)
     auto emit = [&](int y, int xx, float mt, float me) {
         if (xx >= w) return;
-        const float hi = fmaxf(me, mt), lo = fminf(me, mt);
+        const bool edge = me > mt;                  // selects, not fmaxf/fminf: no canonicalising ops
+        const float hi = edge ? me : mt, lo = edge ? mt : me;
         // row offset is wave-uniform (soffset), column offset per lane
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hi * (me > mt ? we : wt)), orsrc,
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hi * (edge ? we : wt)), orsrc,
                                               xx * 4, (y - ys) * ostride4, 0);
         // refine in fp64 when the class is uncertain: lo within the fp32
         // error band of hi (never for all-zero windows); every pixel when

@@ -443,7 +443,7 @@ DCTE_HD void dct16_odd_sc(const float d[8], float& m, float& mE, float& m2, floa
 DCTE_HD void dct16_tex_sc(const float x[16], float& m, float& mE, float& mA, float& mQ,
                           float& m2)
 {
-    float s[8], d[8], X[16];
+    float s[8], d[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) {
         s[j] = x[j] + x[15 - j];
@@ -458,6 +458,7 @@ DCTE_HD void dct16_tex_sc(const float x[16], float& m, float& mE, float& mA, flo
 #if DCTE_ODD16SC
     dct16_odd_sc<false>(d, m, mE, m2);
 #else
+    float X[16];
     dct16_odd_fast(d, X);
 #pragma unroll
     for (int q = 1; q < 16; q += 4) m = fmaxf(fmaxf(m, fabsf(X[q])), fabsf(X[q + 2]));

@@ -202,7 +202,7 @@ struct Cols<16> {
     template <int O>
     DCTE_HD_MEMBER void run(const float (&ring)[16][4], int q, float& mt, float& me)
     {
-        float col[16], X[16];
+        float col[16];
         mt = 0.0f;
         me = 0.0f;
 #if DCTE_SC16
@@ -246,6 +246,7 @@ struct Cols<16> {
             dct16_tex_sc(col, mt, mE, mA, mQ, m2);
         }
 #else
+        float X[16];
         if (q == 0) {
             // exact integer row sums: centre on one of its own samples (exact)
             // so no large partial sum forms; X0 is the DC (excluded), X1 = C01

@@ -157,8 +157,9 @@ __global__ __launch_bounds__(kShiftThreads) void dcte_seam_shift(const SeamParam
 __device__ __forceinline__ void emit_pixel(const SeamParams& p, float mt, float me, float* dst,
                                            unsigned fix_index)
 {
-    const float hi = fmaxf(me, mt), lo = fminf(me, mt);
-    *dst = hi * (me > mt ? p.we : p.wt);        // the map kernel's decision (dcte_map emit)
+    const bool edge = me > mt;                      // as in dcte_map's emit
+    const float hi = edge ? me : mt, lo = edge ? mt : me;
+    *dst = hi * (edge ? p.we : p.wt);        // the map kernel's decision (dcte_map emit)
     if ((p.we != p.wt && lo > (1.0f - p.tie_tau) * hi) || p.tie_tau >= 1.0f) {
         const unsigned k = atomicAdd(p.fix_count, 1u);
         if (k < p.fix_cap) p.fix_list[k] = fix_index;
