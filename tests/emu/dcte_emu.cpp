@@ -39,4 +39,23 @@ int emu_energy_map(const uint8_t* px, int w, int h, int bpp, size_t rowstride, i
         }
     return 0;
 }
+
+// The second (column) pass alone on a ring of row-transform outputs, oldest
+// row first: ring[j * CH + k] for N = 2, 4, 8 (CH = N); N = 16 takes the four
+// channels of wave q (ring[j * 4 + c], channel c = k1 4c + {0,2,1,3}[q]).
+// Returns the pass's (m_t, m_e) in hat units.
+int emu_cols(int n, const float* ring, int q, float* mt, float* me)
+{
+    switch (n) {
+    case 2: { float r[2][2]; for (int i = 0; i < 4; i++) r[i / 2][i % 2] = ring[i];
+              Cols<2>::run<0>(r, 0, *mt, *me); return 0; }
+    case 4: { float r[4][4]; for (int i = 0; i < 16; i++) r[i / 4][i % 4] = ring[i];
+              Cols<4>::run<0>(r, 0, *mt, *me); return 0; }
+    case 8: { float r[8][8]; for (int i = 0; i < 64; i++) r[i / 8][i % 8] = ring[i];
+              Cols<8>::run<0>(r, 0, *mt, *me); return 0; }
+    case 16: { float r[16][4]; for (int i = 0; i < 64; i++) r[i / 4][i % 4] = ring[i];
+               Cols<16>::run<0>(r, q, *mt, *me); return 0; }
+    default: return -1;
+    }
+}
 }
