@@ -1,29 +1,36 @@
-"""Bench: DCT energy map, 16384^2 RGB per GPU, N = 8 (BASELINE.json configs[2..3]).
+"""Bench: DCT energy map of a 16384^2 RGB frame, N = 8 (BASELINE.json configs[2..3]).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 8] [--size 16384]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 8] [--size 16384] [--weak]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-One process per GPU.  A "step" is one pass of the hot path over one frame
-band: the row-band halo exchange (RCCL over xGMI, world > 1) overlapped with
-the interior rows, then the halo rows -- all on HBM-resident input, output
-left in HBM.  Weak scaling: every rank owns 16384 rows x 16384 columns of a
-(world * 16384) x 16384 RGB frame, so N=1 is exactly the 16384^2 config.
+One process per GPU.  With --gpus N > 1 and no launcher around it (WORLD_SIZE
+unset), bench.py starts its N rank processes itself before anything touches a
+GPU, then exits with their status.
+
+A "step" is one pass of the hot path over the frame: every rank maps its row
+band of ONE size x size frame (strong scaling, BASELINE configs[3]) -- the
+halo rows exchanged with the neighbour ranks (RCCL point-to-point over xGMI)
+while the interior rows run, then the halo-dependent rows.  Input resident in
+HBM, output left in HBM.  --weak gives every rank its own size x size band of
+a (N * size) x size frame instead.
 
 Prints ONE JSON line (rank 0).  `value` = Mpx/s over all ranks.  `roofline`
-prices the map kernel (dcte_map<8,RGB>) against the 8 TB/s HBM roof with the
-algorithmic 7 B/px (3 B in + 4 B out), timed by HIP events around that
-kernel alone (dcte_profile_read); the binding roof is the VALU, reported in
-`valu`.  `cpu_baseline` times the oracle (bit-identical restatement of the
-reference path) on this host's cores over a bounded sample of the frame.
+prices the map kernel (dcte_map<N,RGB>) against the 8 TB/s HBM roof with the
+algorithmic 7 B/px (3 B in + 4 B out), timed by HIP events around each launch
+on the launch stream (dcte_profile_read); the binding roof is the VALU,
+reported in `valu`.  `cpu_baseline` times the reference's own transforms
+(oracle/_ref, src/fft2d compiled unmodified) on this host's cores over a
+bounded sample of the frame; `host_path` times the plug-in's real call
+(host frame -> dcte_energy_map -> host map, PCIe-inclusive).
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-sys.path[:0] = [os.path.join(ROOT, "dct-carver_amd"), os.path.join(ROOT, "tests")]
 
 METRIC = "Mpixels/sec DCT-energy-map on 16384² RGB; % MI355X HBM roofline at 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0
@@ -31,7 +38,7 @@ HBM_PEAK_GBS = 8000.0
 VALU_PEAK_LANE_OPS = 256 * 4 * 64 / 2 * 2.4e9
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -41,54 +48,215 @@ def parse():
     ap.add_argument("--edges", type=float, default=0.3)
     ap.add_argument("--textures", type=float, default=0.7)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rows", type=int, default=8192)
+    ap.add_argument("--cpu-rows", type=int, default=0,
+                    help="output rows of the CPU-baseline sample (0: sized to ~15 s of CPU work)")
+    ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: stage halos through host memory (rehearsal of the N>1 path "
                          "on a box with fewer GPUs than ranks)")
-    ap.add_argument("--strong", action="store_true",
-                    help="strong scaling: one fixed size x size frame split into row bands "
-                         "over the ranks (BASELINE.json configs[3]) instead of size x size per rank")
+    ap.add_argument("--weak", action="store_true",
+                    help="weak scaling: every rank owns its own size x size band of a "
+                         "(N * size) x size frame")
     ap.add_argument("--check", action="store_true",
                     help="after timing, recompute every band from regenerated rows (no "
                          "exchange) and require bit-equality")
-    return ap.parse_args()
+    ap.add_argument("--cpu-rehearsal", action="store_true",
+                    help="no GPU: launch the ranks, split a --size frame into bands and "
+                         "exchange the halos over gloo on CPU tensors, check them against "
+                         "the global frame (tests/test_bench_launch.py)")
+    return ap.parse_args(argv)
+
+
+# ------------------------------------------------------------------ launcher
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """Start n rank processes of this script (RANK/LOCAL_RANK/WORLD_SIZE and a
+    127.0.0.1 rendezvous in their environment) and wait for them.  Runs before
+    this process touches a GPU; children are started, never exec'd into.
+    Returns the first non-zero exit status (the others are then stopped)."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc if rc >= 0 else 128 - rc
+
+
+# ------------------------------------------------------------------ baselines
+def cpu_threads():
+    """Host threads this process may use: the CPUs it is allowed to run on,
+    capped by OMP_NUM_THREADS when the environment sets it (the GPU box gives
+    one GPU's job a 16-CPU share of the host)."""
+    allowed = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(allowed, int(env))) if env and env.isdigit() else max(1, allowed)
 
 
 def cpu_baseline(frame_rows_host, W, n, e, t, sample_rows):
-    """Oracle over the first `sample_rows` output rows of the frame, on this
-    host's cores (OpenMP), plus the reference transforms on 1 core."""
+    """The reference path on the host cores over the first `sample_rows`
+    output rows of the bench frame: the reference's own transforms
+    (oracle/_ref = src/fft2d compiled unmodified + the restated dct.c /
+    render.c glue, OpenMP over rows), and the port (oracle/dcte_oracle.c,
+    bit-identical to them) beside it."""
     import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as O
-    threads = min(16, os.cpu_count() or 1)
-    O.lib()
+    threads = cpu_threads()
     img = frame_rows_host
+    res = None
+    if O.ref_available():
+        L = np.ascontiguousarray(O.luma_plane(img))          # liblqr's rcache: luma once
+        t0 = time.perf_counter()
+        O.ref_energy_map_luma_rows(L, n, e, t, y0=0, y1=sample_rows, h=L.shape[0],
+                                   nthreads=threads)
+        dt = time.perf_counter() - t0
+        res = {"value": round(sample_rows * W / dt / 1e6, 3), "unit": "Mpx/s", "cores": threads,
+               "kind": "reference",
+               "sample": f"output rows 0..{sample_rows - 1} x {W} cols of the bench frame "
+                         f"(N={n}, e={e}, t={t}): the reference's own src/fft2d transforms "
+                         f"(oracle/_ref) per pixel in liblqr build order, luma precomputed, "
+                         f"OpenMP over rows on {threads} threads, {dt:.2f} s wall = "
+                         f"{dt * threads:.1f} thread-s"}
     t0 = time.perf_counter()
     O.energy_map(img, n, e, t, y0=0, y1=sample_rows, nthreads=threads)
-    dt = time.perf_counter() - t0
-    res = {"value": round(sample_rows * W / dt / 1e6, 3), "unit": "Mpx/s", "cores": threads,
-           "kind": "port",
-           "sample": f"rows 0..{sample_rows - 1} x {W} cols of the bench frame (N={n}, "
-                     f"e={e}, t={t}); oracle/dcte_oracle.c (bit-identical to the reference "
-                     f"transforms), OpenMP over rows, {dt:.2f} s wall = {dt * threads:.1f} "
-                     f"thread-s",
-           "host_cpus": os.cpu_count()}
-    if O.ref_available():
-        rows1 = max(8, sample_rows // 2)
-        L = O.luma_plane(img[:rows1 + n])
-        sub = np.ascontiguousarray(L)
-        t0 = time.perf_counter()
-        O.ref_energy_map_luma(sub, n, e, t)
-        d1 = time.perf_counter() - t0
-        res["reference_1core"] = {
-            "value": round(sub.shape[0] * W / d1 / 1e6, 3), "unit": "Mpx/s", "cores": 1,
-            "kind": "reference",
-            "sample": f"{sub.shape[0]} rows x {W}: the reference's own src/fft2d transforms "
-                      f"(oracle/_ref) in liblqr build order, luma precomputed, serial, {d1:.2f} s"}
+    dp = time.perf_counter() - t0
+    port = {"value": round(sample_rows * W / dp / 1e6, 3), "unit": "Mpx/s", "cores": threads,
+            "kind": "port",
+            "sample": f"same rows; oracle/dcte_oracle.c (bit-identical restatement incl. the "
+                      f"luma), {dp:.2f} s wall"}
+    if res is None:
+        res = port
+    else:
+        res["port"] = port
+    res["host_cpus"] = os.cpu_count()
+    res["cpus_allowed"] = (len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity")
+                           else os.cpu_count())
     return res
 
 
+def host_path(ctx, frame_dev, n, e, t, iters=3):
+    """The plug-in's own call: a pageable host frame (GIMP's rgb buffer,
+    src/render.c:159-173) -> dcte_energy_map -> a pageable host map; the library
+    page-locks both for the call and pipelines H2D / map / D2H in row chunks."""
+    import numpy as np
+    px = frame_dev.cpu().numpy()
+    H, W = px.shape[:2]
+    out = np.empty((H, W), np.float32)
+    ctx.energy_map(px, n, e, t, out=out)
+    ts = []
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        ctx.energy_map(px, n, e, t, out=out)
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    med = ts[len(ts) // 2]
+    return {"value": round(H * W / med / 1e9, 2), "unit": "Gpx/s", "ms": round(med * 1e3, 2),
+            "best_ms": round(ts[0] * 1e3, 2), "iters": iters,
+            "bytes_h2d": int(px.nbytes), "bytes_d2h": int(out.nbytes),
+            "what": f"{H}x{W} RGB pageable host frame -> dcte_energy_map -> host map "
+                    f"(PCIe-inclusive; page-locked per call, 2048-row chunk pipeline)"}
+
+
+def pmc_figures(n, W, px_per_rank):
+    """Counter figures for dcte_map<n,RGB> from the committed rocprofv3 --pmc
+    summary (profiles/pmc_summary.json, tools/pmc_summary.py), per pixel, so a
+    rank is charged for ITS band: HBM bytes (FETCH_SIZE x 2 on gfx950 +
+    WRITE_SIZE, MI355X_MICROARCH.md §HBM) and VALU lane-ops (SQ_INSTS_VALU x 64)."""
+    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(p) as f:
+            allsum = json.load(f)
+    except (OSError, ValueError):
+        return {}
+    best = None
+    for key, v in allsum.items():
+        if not key.startswith(f"dcte_map<{n},3>@"):
+            continue
+        if best is None or abs(v["frame"][1] - W) < abs(best["frame"][1] - W):
+            best = v
+    if best is None:
+        return {}
+    px = best["pixels"]
+    out = {"valu_lane_ops_per_px": best.get("valu_lane_ops_per_px"),
+           "pmc_frame": best["frame"], "pmc_round": best.get("round")}
+    if best.get("hbm_bytes_per_launch"):
+        out["hbm_bytes_per_px"] = best["hbm_bytes_per_launch"] / px
+        out["traffic"] = round(out["hbm_bytes_per_px"] * px_per_rank)
+    return out
+
+
+def cpu_rehearsal(args):
+    """The rank/band/halo plumbing of a step without a GPU: every rank holds
+    its band of the global frame with the halo rows zeroed, exchanges halos
+    over gloo, and checks that its buffer equals the global frame's rows."""
+    import torch
+    import torch.distributed as dist
+    from dctenergy import dist as D
+    from dctenergy import synth
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    n, S = args.n, args.size
+    H, W = (world * S, S) if args.weak else (S, S)
+    band = (D.make_band(H, rank, world, n, rows_per_rank=S) if args.weak
+            else D.make_band(H, rank, world, n))
+    buf = torch.zeros((band.rows, W, 3), dtype=torch.uint8)
+    buf[band.top:band.top + band.own] = synth.natural_rows(band.Y0, band.own, W, 3, device="cpu")
+    for r in (D.exchange_halos(buf, band) if world > 1 else []):
+        r.wait()
+    ok = torch.tensor([int(torch.equal(buf, synth.natural_rows(band.row0, band.rows, W, 3,
+                                                               device="cpu")))])
+    rows = torch.tensor([band.own])
+    if world > 1:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        everyone = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(everyone, rows)
+        rows_all = [int(v) for v in everyone]
+    else:
+        rows_all = [band.own]
+    if rank == 0:
+        print(json.dumps({"rehearsal": "cpu", "n_gpus": world,
+                          "scaling": "weak" if args.weak else "strong",
+                          "global_frame": [H, W], "rows_per_rank": rows_all,
+                          "check_halo_exact": bool(ok.item())}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0 if ok.item() else 1
+
+
+# ------------------------------------------------------------------ bench
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+
+    sys.path.insert(0, os.path.join(ROOT, "dct-carver_amd"))
+    if args.cpu_rehearsal:
+        sys.exit(cpu_rehearsal(args))
     import torch
     import torch.distributed as dist
 
@@ -100,22 +268,22 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print("bench: --gpus N > 1 needs torch.distributed.run (one process per GPU)",
-                  file=sys.stderr)
-            sys.exit(2)
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     ndev = torch.cuda.device_count()
     gpu = local % max(1, ndev)          # == local on a full node
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
+    gloo = args.dist_backend == "gloo"
     if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
+        if gloo:
             dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     n, S = args.n, args.size
-    if args.strong:
+    strong = not args.weak
+    if strong:
         H, W = S, S
         band = D.make_band(H, rank, world, n)
     else:
@@ -131,11 +299,8 @@ def main():
     out = torch.empty((band.own, W), dtype=torch.float32, device=dev)
     torch.cuda.synchronize()
 
-    # a context over the visible devices (state is created lazily, only on the
-    # device this rank uses); device index = this rank's local device
     ctx = dctenergy.Context(ngpus=0)
     dev_index = gpu
-
     stream = torch.cuda.current_stream(dev).cuda_stream
     e, t = args.edges, args.textures
     i0, i1 = band.interior()
@@ -148,12 +313,10 @@ def main():
                               n, e, t, out[y0 - band.Y0:].data_ptr(), out.stride(0), stream,
                               dev_index)
 
-    host_buf = None
-    if world > 1 and args.dist_backend == "gloo":
-        host_buf = torch.empty(buf.shape, dtype=torch.uint8, pin_memory=True)
+    host_buf = torch.empty(buf.shape, dtype=torch.uint8, pin_memory=True) if world > 1 and gloo else None
 
     def step():
-        if world > 1 and host_buf is not None:
+        if host_buf is not None:
             # rehearsal path: halo rows via host memory and gloo
             run_rows(i0, i1)
             t0_, o_ = band.top, band.own
@@ -191,23 +354,24 @@ def main():
     elapsed = time.perf_counter() - t0
     launches, kern_ms = ctx.profile_read()
     ctx.set_option(dctenergy.DCTE_OPT_PROFILE, 0)
-    # interior launch is the dominant kernel; edge launches are a few rows
-    stats = torch.tensor([elapsed], dtype=torch.float64,
-                         device="cpu" if args.dist_backend == "gloo" else dev)
+    stats = torch.tensor([elapsed, kern_ms / args.steps], dtype=torch.float64,
+                         device="cpu" if gloo else dev)
     if world > 1:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
     elapsed = float(stats[0])
+    kernel_ms_max_rank = float(stats[1])
 
     px_per_rank = band.own * W
-    total_px = px_per_rank * world * args.steps
-    value = total_px / elapsed / 1e6
+    total_px = H * W if strong else px_per_rank * world
+    value = total_px * args.steps / elapsed / 1e6
     ms_per_step = elapsed * 1e3 / args.steps
 
-    # roofline of the map kernel: algorithmic bytes per launch / mean launch time
+    # roofline of the map kernel on this rank: algorithmic bytes per step over
+    # the summed launch time of its map launches per step (interior + edges)
     kernel_ms_per_step = kern_ms / args.steps
     bytes_per_step = px_per_rank * (3 + 4)
     achieved_gbs = bytes_per_step / (kernel_ms_per_step * 1e-3) / 1e9
-    pmc = _pmc(n, S)
+    pmc = pmc_figures(n, W, px_per_rank)
     valu_per_px = pmc.get("valu_lane_ops_per_px")
     valu_rate = (px_per_rank * valu_per_px / (kernel_ms_per_step * 1e-3)) if valu_per_px else None
 
@@ -222,7 +386,7 @@ def main():
                               stream, dev_index)
         torch.cuda.synchronize()
         ok = torch.tensor([1 if (torch.equal(ref_out, out) and torch.equal(ref_in, buf)) else 0],
-                          dtype=torch.int64, device="cpu" if args.dist_backend == "gloo" else dev)
+                          dtype=torch.int64, device="cpu" if gloo else dev)
         if world > 1:
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         check = bool(ok.item())
@@ -237,15 +401,15 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "strong" if args.strong else "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic natural-like RGB (counter-hash noise), generated on device",
             "config": {
-                "workload": (f"{H}x{W} RGB frame split into {world} row band(s)" if args.strong
+                "workload": (f"{H}x{W} RGB frame split into {world} row band(s)" if strong
                              else f"{S}x{S} RGB per GPU (global {H}x{W} frame, row bands)")
                             + f", N={n}, edges={e}, textures={t}, liblqr-callback semantics",
-                "frame_per_gpu": [band.own, W], "global_frame": [H, W], "block": n,
+                "rows_per_gpu": band.own, "global_frame": [H, W], "block": n,
                 "parallelism": f"row-band x{world}" + (", RCCL P2P halo exchange overlapped"
                                                         " with interior rows" if world > 1 else ""),
             },
@@ -255,13 +419,19 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
-                "traffic": pmc.get("hbm_bytes_per_launch"),
+                "traffic": pmc.get("traffic"),
+                "traffic_source": (f"rocprofv3 PMC of dcte_map<{n},3> at {pmc['pmc_frame'][0]}x"
+                                   f"{pmc['pmc_frame'][1]} ({pmc['pmc_round']}), HBM bytes per "
+                                   f"pixel x this rank's {px_per_rank} px") if "traffic" in pmc
+                else None,
                 "kernel": f"dcte_map<{n},3>",
                 "kernel_ms": round(kernel_ms_per_step, 4),
+                "kernel_ms_max_rank": round(kernel_ms_max_rank, 4),
                 "algorithmic_bytes_per_px": 7,
+                "px_per_rank": px_per_rank,
                 "launches_timed": launches,
-                "note": "binding roof is VALU (see valu); HBM frac ceiling for this "
-                        "computation is ~20 % (DESIGN.md §4)",
+                "note": "rank 0's map launches; binding roof is VALU (see valu) -- the HBM "
+                        "fraction ceiling of this computation is ~24 % (DESIGN.md §4)",
             },
             "valu": {
                 "lane_ops_per_px": valu_per_px,
@@ -274,28 +444,21 @@ def main():
         }
         if check is not None:
             res["check_bands_bit_exact"] = check
-        if world > 1 and args.dist_backend != "nccl":
-            res["config"]["parallelism"] += f" (halo via {args.dist_backend} rehearsal)"
+        if world > 1 and gloo:
+            res["config"]["parallelism"] += " (halo via gloo rehearsal)"
+            if ndev < world:
+                res["config"]["parallelism"] += f"; {world} ranks share {ndev} GPU(s)"
+        if world == 1 and not args.no_host_path:
+            res["host_path"] = host_path(ctx, buf, n, e, t)
         if world == 1 and not args.no_cpu_baseline:
-            host = buf[:args.cpu_rows + n].cpu().numpy()
-            res["cpu_baseline"] = cpu_baseline(host, W, n, e, t, args.cpu_rows)
+            rows = args.cpu_rows or max(64, S // 2)
+            rows = min(rows, H)
+            host = buf[:min(H, rows + n)].cpu().numpy()
+            res["cpu_baseline"] = cpu_baseline(host, W, n, e, t, rows)
         print(json.dumps(res), flush=True)
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
-
-
-def _pmc(n, S):
-    """Counter-derived figures for dcte_map<n,3> at S x S from the committed
-    rocprofv3 --pmc summary (profiles/pmc_summary.json, tools/pmc_summary.py):
-    HBM bytes per launch (FETCH_SIZE x 2 on gfx950 + WRITE_SIZE,
-    MI355X_MICROARCH.md §HBM) and VALU lane-ops per pixel (SQ_INSTS_VALU x 64)."""
-    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    try:
-        with open(p) as f:
-            return json.load(f)[f"dcte_map<{n},3>@{S}"]
-    except Exception:
-        return {}
 
 
 if __name__ == "__main__":

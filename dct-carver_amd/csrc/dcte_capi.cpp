@@ -62,6 +62,32 @@ struct Device {
     std::vector<hipEvent_t> ev;    // host path: chunk hand-offs
 };
 
+// Restores the calling thread's current device on every return path of a
+// public entry point: the library switches devices internally (hipSetDevice),
+// and a caller such as PyTorch allocates on whatever device is current.
+struct DeviceGuard {
+    int prev = -1;
+    DeviceGuard()
+    {
+        if (hipGetDevice(&prev) != hipSuccess) {
+            prev = -1;
+            (void)hipGetLastError();
+        }
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
+// one buffer resource addresses a frame's readable bytes: they must span < 4 GiB
+bool span_ok(int h, long long rowstride, int w, int bpp)
+{
+    return (long long)(h - 1) * rowstride + (long long)w * bpp + 6 < (1LL << 32);
+}
+
 }  // namespace
 
 struct ProfEvent {
@@ -463,16 +489,17 @@ int dcte_device_count(void)
 
 int dcte_create(dcte_ctx** out, int ngpus, unsigned flags)
 {
-    (void)flags;
-    if (!out || ngpus < 0) return DCTE_EINVAL;
+    if (!out || ngpus < 0 || (flags & ~DCTE_CREATE_SAME_DEVICE)) return DCTE_EINVAL;
     *out = nullptr;
     int count = dcte_device_count();
     if (count <= 0) return DCTE_ENODEV;
-    if (ngpus == 0 || ngpus > count) ngpus = count;
+    const bool same = (flags & DCTE_CREATE_SAME_DEVICE) != 0;
+    if (ngpus == 0) ngpus = same ? 1 : count;
+    if (!same && ngpus > count) ngpus = count;
     dcte_ctx* ctx = new (std::nothrow) dcte_ctx;
     if (!ctx) return DCTE_ENOMEM;
     ctx->devs.resize(ngpus);
-    for (int i = 0; i < ngpus; i++) ctx->devs[i].id = i;
+    for (int i = 0; i < ngpus; i++) ctx->devs[i].id = same ? 0 : i;
     const char* tau = getenv("DCTE_TIE_TAU");
     if (tau && *tau) ctx->tie_tau = atof(tau);
     *out = ctx;
@@ -481,6 +508,7 @@ int dcte_create(dcte_ctx** out, int ngpus, unsigned flags)
 
 void dcte_destroy(dcte_ctx* ctx)
 {
+    DeviceGuard guard_;
     if (!ctx) return;
     for (Device& d : ctx->devs) {
         if (d.id < 0) continue;
@@ -537,6 +565,7 @@ int dcte_energy_map_device(dcte_ctx* ctx, int device, const void* d_px, long lon
                            int n, float edges, float textures, int semantics, float* d_out,
                            long long out_stride, void* stream)
 {
+    DeviceGuard guard_;
     if (!ctx || device < 0 || device >= (int)ctx->devs.size()) return DCTE_EINVAL;
     return run_device(ctx, ctx->devs[device], d_px, rowstride, w, h, bpp, in_row0, in_rows, y0,
                       y1, n, edges, textures, semantics, d_out, out_stride, (hipStream_t)stream);
@@ -548,6 +577,7 @@ int dcte_seam_carve_device(dcte_ctx* ctx, int device, const void* d_px, long lon
                            float* d_map_out, long long map_out_stride, int n, float edges,
                            float textures, int semantics, void* stream)
 {
+    DeviceGuard guard_;
     if (!ctx) return DCTE_EINVAL;
     DCTE_ARG(ctx, device >= 0 && device < (int)ctx->devs.size());
     DCTE_ARG(ctx, valid_n(n) && valid_sem_bpp(semantics, bpp) && w >= 2 && h >= 1);
@@ -560,6 +590,11 @@ int dcte_seam_carve_device(dcte_ctx* ctx, int device, const void* d_px, long lon
     FixScratch* f = nullptr;
     const size_t npix = (size_t)(w - 1) * (size_t)h;
     if (npix >= (1ULL << 32)) return DCTE_ERANGE;
+    // the shift and band kernels address both frames through 32-bit buffer offsets
+    if (!span_ok(h, rowstride, w, bpp) || !span_ok(h, out_rowstride, w - 1, bpp)) {
+        ctx->last_error = "frame spans 4 GiB or more";
+        return DCTE_ERANGE;
+    }
     int rc = ensure_fix(ctx, d, s, npix, &f);
     if (rc) return rc;
     const double scale = weight_scale(n, semantics);
@@ -599,6 +634,7 @@ int dcte_energy_points_device(dcte_ctx* ctx, int device, const void* d_px, long 
                               float edges, float textures, int semantics, float* d_out,
                               void* stream)
 {
+    DeviceGuard guard_;
     if (!ctx) return DCTE_EINVAL;
     DCTE_ARG(ctx, device >= 0 && device < (int)ctx->devs.size());
     DCTE_ARG(ctx, valid_n(n) && valid_sem_bpp(semantics, bpp) && w >= 1 && h >= 1 && count >= 0);
@@ -645,6 +681,7 @@ int dcte_energy_points(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, 
                        const int* xy, int count, int n, float edges, float textures, int semantics,
                        float* out)
 {
+    DeviceGuard guard_;
     if (!ctx) return DCTE_EINVAL;
     DCTE_ARG(ctx, valid_n(n) && valid_sem_bpp(semantics, bpp) && w >= 1 && h >= 1 && count >= 0);
     DCTE_ARG(ctx, rowstride >= (size_t)w * bpp);
@@ -682,6 +719,7 @@ int dcte_energy_points(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, 
 int dcte_seam_find_device(dcte_ctx* ctx, int device, const float* d_map, long long map_stride,
                           int w, int h, int* d_seam, void* stream)
 {
+    DeviceGuard guard_;
     if (!ctx) return DCTE_EINVAL;
     DCTE_ARG(ctx, device >= 0 && device < (int)ctx->devs.size());
     DCTE_ARG(ctx, d_map && d_seam && w >= 1 && h >= 1 && map_stride >= w);
@@ -745,6 +783,7 @@ int dcte_seam_find_device(dcte_ctx* ctx, int device, const float* d_map, long lo
 
 int dcte_seam_find(dcte_ctx* ctx, const float* map, int w, int h, int* seam)
 {
+    DeviceGuard guard_;
     if (!ctx) return DCTE_EINVAL;
     DCTE_ARG(ctx, map && seam && w >= 1 && h >= 1);
     Device& d = ctx->devs[0];
@@ -774,6 +813,7 @@ int dcte_carve(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t r
                float edges, float textures, int semantics, int seams, int transposed,
                uint8_t* out, int* seam_cols)
 {
+    DeviceGuard guard_;
     if (!ctx) return DCTE_EINVAL;
     DCTE_ARG(ctx, px && out && valid_n(n) && valid_sem_bpp(semantics, bpp) && w > 0 && h > 0);
     DCTE_ARG(ctx, rowstride >= (size_t)w * bpp);
@@ -858,6 +898,7 @@ int dcte_carve(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t r
 int dcte_energy_map(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride,
                     int n, float edges, float textures, int semantics, int transposed, float* out)
 {
+    DeviceGuard guard_;
     if (!ctx) return DCTE_EINVAL;
     DCTE_ARG(ctx, px && out && valid_n(n) && valid_sem_bpp(semantics, bpp) && w > 0 && h > 0);
     DCTE_ARG(ctx, rowstride >= (size_t)w * bpp);
@@ -878,6 +919,7 @@ int dcte_energy_image_u8(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp
                          size_t rowstride, int n, float edges, float textures, int semantics,
                          int mode, int channels, uint8_t* out)
 {
+    DeviceGuard guard_;
     if (!ctx) return DCTE_EINVAL;
     DCTE_ARG(ctx, px && out && valid_n(n) && valid_sem_bpp(semantics, bpp) && w > 0 && h > 0);
     DCTE_ARG(ctx, rowstride >= (size_t)w * bpp && valid_norm(mode, channels));
@@ -938,6 +980,7 @@ extern "C" {
 
 int dcte_normalize_u8(dcte_ctx* ctx, const float* E, size_t n, int mode, int channels, uint8_t* out)
 {
+    DeviceGuard guard_;
     if (!ctx || !E || !out || n == 0 || !valid_norm(mode, channels)) return DCTE_EINVAL;
     Device& d = ctx->devs[0];
     int rc = ensure_stream(ctx, d);
@@ -957,6 +1000,7 @@ int dcte_normalize_u8(dcte_ctx* ctx, const float* E, size_t n, int mode, int cha
 int dcte_minmax_device(dcte_ctx* ctx, int device, const float* d_E, long long n, float* d_minmax,
                        void* stream)
 {
+    DeviceGuard guard_;
     if (!ctx || device < 0 || device >= (int)ctx->devs.size() || !d_E || !d_minmax || n <= 0)
         return DCTE_EINVAL;
     Device& d = ctx->devs[device];
@@ -972,6 +1016,7 @@ int dcte_normalize_u8_device(dcte_ctx* ctx, int device, const float* d_E, long l
                              const float* d_minmax, int mode, int channels, uint8_t* d_out,
                              void* stream)
 {
+    DeviceGuard guard_;
     if (!ctx || device < 0 || device >= (int)ctx->devs.size() || !d_E || !d_minmax || !d_out ||
         n <= 0 || !valid_norm(mode, channels))
         return DCTE_EINVAL;
@@ -982,6 +1027,7 @@ int dcte_normalize_u8_device(dcte_ctx* ctx, int device, const float* d_E, long l
 
 int dcte_profile_read(dcte_ctx* ctx, long long* launches, double* kernel_ms)
 {
+    DeviceGuard guard_;
     if (!ctx || !launches || !kernel_ms) return DCTE_EINVAL;
     double total = 0.0;
     int rc = DCTE_OK;

@@ -1,6 +1,6 @@
 // dcte_kernels.hip -- gfx950 kernels for the dct-carver energy map.
 //
-// What is computed (reference: src/render.c:134-157 + src/dct.c:93-126):
+// What is computed (reference: src/render.c:134-157 + src/dct.c:77-110):
 // for every pixel (x, y) the N x N luma window with offsets -(N/2-1)..N/2 in
 // both axes (replicate-clamped at the image border), its 2-D DCT-II, and
 //     E = m_e > m_t ? m_e * edges : m_t * textures
@@ -368,7 +368,7 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
 // One wave per flagged pixel: the N*N window is gathered in parallel (one
 // element per lane), each 1-D pass of the reference transform runs on N lanes
 // (one lane per line, the reference's own operation sequence, fp64, in LDS),
-// and the last-maximum scan of src/dct.c:116-124 becomes an exact reduction:
+// and the last-maximum scan of src/dct.c:100-108 becomes an exact reduction:
 // M = max |C| over the non-DC coefficients, and the winner is the LARGEST
 // linear index k1*N + k2 with |C| == M (that is what "max <= currval" keeps).
 constexpr int kFixWaves = 4;

@@ -8,7 +8,7 @@
 // exactly  L / 1275000  with the integer  L = 1063 R + 3576 G + 361 B  (grey:
 // L = 5000 v), 0 <= L <= 1275000.  The kernels work on L - 637500, an exact
 // fp32 integer in [-637500, 637500]; the bias only moves the DC coefficient,
-// which the energy never looks at (src/dct.c:119, "k1 || k2").
+// which the energy never looks at (src/dct.c:103, "k1 || k2").
 #pragma once
 
 #if defined(__HIPCC__)

@@ -14,7 +14,7 @@
 // unnormalised family (N = 2, 4: ddct2d, src/fft2d/fftsg2d.c:204-209).
 // Then every 2-D coefficient is C[k1][k2] * S with one global S (N for the
 // orthonormal family, 1 for the unnormalised one), so comparisons between
-// coefficients -- all that the weighted max needs (src/dct.c:112-126) -- are
+// coefficients -- all that the weighted max needs (src/dct.c:96-110) -- are
 // unaffected, and the kernel folds 1/S and the luma scale into the weights.
 //
 // Exactness.  Inputs are integer-valued luma samples biased into

@@ -7,7 +7,7 @@
 // reference's first index, src/fft2d/shrtdct.c:62-89) of the lane's output
 // column; slot O is the oldest.  A column pass runs the second-pass transforms
 // (along y) over the ring and folds |C| into
-//     m_e = max(|C01|, |C10|)   (edge atoms, src/dct.c:34-41 LUT)
+//     m_e = max(|C01|, |C10|)   (edge atoms, src/dct.c:18-25 LUT)
 //     m_t = max over the other non-DC coefficients.
 #pragma once
 

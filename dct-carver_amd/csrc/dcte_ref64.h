@@ -2,7 +2,7 @@
 //
 // The fast fp32 path (dcte_math.h) agrees with the reference to ~1e-6
 // relative, but the edge/texture class of a pixel is a comparison
-// (src/dct.c:119-125: last maximum wins, so "edge" iff max|C01|,|C10| is
+// (src/dct.c:100-109: last maximum wins, so "edge" iff max|C01|,|C10| is
 // strictly larger than every texture atom).  Pixels whose two candidates are
 // within the fp32 error band are recomputed here in fp64, in the reference's
 // own operation order, so the class -- and the value -- equal the reference's:
@@ -14,7 +14,7 @@
 //                src/fft2d/fftsg.c:349-402 (cftx020, dctsub), twiddles from
 //                makect (fftsg.c:724-740) evaluated on the host with libm and
 //                passed in, exactly as the reference evaluates them
-//   - max      : src/dct.c:112-126
+//   - max      : src/dct.c:96-110
 // The TU is compiled with -ffp-contract=off so no multiply-add is fused.
 #pragma once
 

@@ -34,6 +34,7 @@ DCTE_OPT_PROFILE = 2
 DCTE_OPT_PIN_HOST = 3
 DCTE_NORM_LQR = 0
 DCTE_NORM_PREVIEW = 1
+DCTE_CREATE_SAME_DEVICE = 1
 
 # every symbol include/dctenergy.h declares
 EXPORTS = ("dcte_abi_version", "dcte_device_count", "dcte_create", "dcte_destroy",
@@ -152,10 +153,13 @@ class Context:
     """One dcte_ctx (a set of devices).  Not thread-safe, like the reference
     callback (src/render.c:140 shares params->data)."""
 
-    def __init__(self, ngpus=0, tie_tau=None):
+    def __init__(self, ngpus=0, tie_tau=None, same_device=False):
+        """same_device: `ngpus` logical devices that are all device 0
+        (DCTE_CREATE_SAME_DEVICE) -- the multi-device host path on one GPU."""
         L = lib()
         h = ctypes.c_void_p()
-        rc = L.dcte_create(ctypes.byref(h), ngpus, 0)
+        rc = L.dcte_create(ctypes.byref(h), ngpus,
+                           DCTE_CREATE_SAME_DEVICE if same_device else 0)
         if rc != DCTE_OK:
             raise DcteError(rc)
         self._h = h

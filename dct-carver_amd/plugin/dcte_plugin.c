@@ -1,5 +1,7 @@
 /* dcte_plugin.c -- see dcte_plugin.h.  One process-wide dcte_ctx, created on
- * first use over DCTE_NGPUS devices (0 / unset = all), destroyed at exit. */
+ * first use over DCTE_NGPUS devices (unset = 1 device, 0 = all visible),
+ * destroyed at exit.  One device by default: a GIMP frame fits one MI355X many
+ * times over, and the single-device path is the one the GPU tests run. */
 #include "dcte_plugin.h"
 
 #include <stdlib.h>
@@ -20,7 +22,7 @@ static dcte_ctx *plugin_ctx(void)
 {
     if (g_ctx_status == 1) {
         const char *ng = getenv("DCTE_NGPUS");
-        g_ctx_status = dcte_create(&g_ctx, ng ? atoi(ng) : 0, 0);
+        g_ctx_status = dcte_create(&g_ctx, ng && *ng ? atoi(ng) : 1, 0);
         if (g_ctx_status == DCTE_OK) atexit(release_ctx);
     }
     return g_ctx_status == DCTE_OK ? g_ctx : NULL;

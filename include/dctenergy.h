@@ -9,10 +9,10 @@
  *   - the per-pixel liblqr energy callback dct_pixel_energy
  *     (src/render.c:134-157, registered at src/render.c:314-315 with radius
  *     N/2 and LQR_ER_LUMA), called W*H times by liblqr's energy build, and
- *     the arithmetic under it: dctNxN (src/dct.c:93-110) ->
+ *     the arithmetic under it: dctNxN (src/dct.c:77-94) ->
  *     ddct8x8s / ddct16x16s / ddct2d (src/fft2d/shrtdct.c:55, :231;
  *     src/fft2d/fftsg2d.c:566) and weighted_max_dct_correlation
- *     (src/dct.c:112-126).  dcte_energy_map computes all W*H callback
+ *     (src/dct.c:96-110).  dcte_energy_map computes all W*H callback
  *     results of one carver build in one call; the plug-in then serves
  *     dct_pixel_energy(x, y, ...) from the returned map.
  *
@@ -28,7 +28,7 @@
  * Errors: every entry point returns DCTE_OK (0) or a negative DCTE_E* code
  * and never exits the process (the reference exit(1)s on OOM,
  * src/fft2d/alloc.c:5-10, and silently leaves the data untransformed for a
- * bad N, src/dct.c:105-108; here a bad N is DCTE_EINVAL).
+ * bad N, src/dct.c:89-92; here a bad N is DCTE_EINVAL).
  *
  * Threading: one context serves one thread at a time (the reference callback
  * is not re-entrant either: it shares params->data, src/render.c:140).
@@ -86,7 +86,12 @@ int dcte_abi_version(void);
 int dcte_device_count(void);
 
 /* Create a context on `ngpus` devices (0 = all visible).  Device memory,
- * streams and kernels are set up lazily on first use.  flags: reserved, 0. */
+ * streams and kernels are set up lazily on first use.  flags: 0, or
+ * DCTE_CREATE_SAME_DEVICE: `ngpus` logical devices that are all physical
+ * device 0 (each with its own streams and buffers), so the multi-device host
+ * path -- band split, halo rows, per-device pipelines, the u8 min/max merge --
+ * can be checked against the 1-device map on a 1-GPU machine. */
+#define DCTE_CREATE_SAME_DEVICE 1u
 int dcte_create(dcte_ctx **ctx, int ngpus, unsigned flags);
 void dcte_destroy(dcte_ctx *ctx);
 

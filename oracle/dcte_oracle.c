@@ -229,10 +229,10 @@ int orc_dct(int n, double *d)
         for (i = 0; i < n; i++) fwd_small(n, d + i, n, c);
         return 0;
     }
-    return -1; /* reference: error() and no transform (src/dct.c:105-108) */
+    return -1; /* reference: error() and no transform (src/dct.c:89-92) */
 }
 
-/* weighted_max_dct_correlation, src/dct.c:112-126: last maximum wins
+/* weighted_max_dct_correlation, src/dct.c:96-110: last maximum wins
  * (max <= currval), DC excluded, class from the edge LUT ((0,1),(1,0)). */
 float orc_weighted_max(int n, const double *d, float edges, float textures)
 {

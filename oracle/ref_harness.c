@@ -12,8 +12,8 @@
  * glue around the transforms are restated below, with the reference's own
  * scratch layout (row-pointer arrays from alloc_2d_double, ip[] / w[] sized
  * as in src/render.c:302-305, ip[0] = 0 once per carver):
- *   - dctNxN dispatch           src/dct.c:93-110
- *   - weighted max + edge LUT   src/dct.c:72-89, 112-126
+ *   - dctNxN dispatch           src/dct.c:77-94
+ *   - weighted max + edge LUT   src/dct.c:10-43, 56-73, 96-110
  *   - window gather + clamp     src/render.c:122-157
  *   - preview gather + luma     src/render.c:31-79 (row-streamed window over
  *                               u8 luma rows, RGB2LUMINANCE src/render.h:5)
@@ -24,7 +24,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
-/* prototypes as declared by the reference at src/dct.c:67-69 */
+/* prototypes as declared by the reference at src/dct.c:51-53 */
 void ddct8x8s(int isgn, double **a);
 void ddct16x16s(int isgn, double **a);
 void ddct2d(int n1, int n2, int isgn, double **a, double *t, int *ip, double *w);
@@ -142,6 +142,38 @@ int ref_energy_map_luma(const double *luma, int w, int h, int n, float edges,
             out[(size_t)y * w + x] = weighted_max(&s, edges, textures);
         }
     scratch_free(&s);
+    return 0;
+}
+
+/* Output rows [y0, y1) of the map of a w*h luma plane, OpenMP over rows with
+ * one scratch per thread (the reference's per-carver scratch,
+ * src/render.c:296-305, is what makes its callback non-re-entrant; each
+ * thread owning one restores re-entrancy without touching the transforms).
+ * The CPU baseline of bench.py: the reference path on the host cores. */
+int ref_energy_map_luma_rows(const double *luma, int w, int h, int n, float edges,
+                             float textures, int y0, int y1, int nthreads, float *out)
+{
+    if (n != 2 && n != 4 && n != 8 && n != 16) return -1;
+    if (y0 < 0 || y1 > h || y0 > y1 || w <= 0) return -1;
+    int r = n / 2;
+#pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1)
+    {
+        ref_scratch s;
+        scratch_init(&s, n);
+#pragma omp for schedule(dynamic, 4)
+        for (int y = y0; y < y1; y++)
+            for (int x = 0; x < w; x++) {
+                for (int i = -r + 1; i <= r; i++)
+                    for (int j = -r + 1; j <= r; j++) {
+                        int ii = clamp_off(x, i, 0, w - 1);
+                        int jj = clamp_off(y, j, 0, h - 1);
+                        s.data[i + r - 1][j + r - 1] = luma[(size_t)(y + jj) * w + (x + ii)];
+                    }
+                dispatch(&s);
+                out[(size_t)(y - y0) * w + x] = weighted_max(&s, edges, textures);
+            }
+        scratch_free(&s);
+    }
     return 0;
 }
 

@@ -82,6 +82,10 @@ def ref():
         R.ref_energy_map_luma.restype = ctypes.c_int
         R.ref_energy_map_luma.argtypes = [_f64p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_float, ctypes.c_float, _f32p]
+        R.ref_energy_map_luma_rows.restype = ctypes.c_int
+        R.ref_energy_map_luma_rows.argtypes = [_f64p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_float, ctypes.c_float, ctypes.c_int,
+                                               ctypes.c_int, ctypes.c_int, _f32p]
         R.ref_window_energy.restype = ctypes.c_float
         R.ref_window_energy.argtypes = [ctypes.c_int, _f64p, ctypes.c_float, ctypes.c_float]
         R.ref_preview_map.restype = ctypes.c_int
@@ -180,6 +184,22 @@ def ref_energy_map_luma(luma, n, edges, textures):
     h, w = luma.shape
     out = np.empty((h, w), np.float32)
     rc = R.ref_energy_map_luma(_ptr(luma, _f64p), w, h, n, edges, textures, _ptr(out, _f32p))
+    if rc != 0:
+        raise ValueError("reference rejected the call")
+    return out
+
+
+def ref_energy_map_luma_rows(luma, n, edges, textures, y0=0, y1=None, h=None, nthreads=1):
+    """Rows [y0, y1) of the reference map of a luma plane whose first `h` rows
+    are the frame (OpenMP over rows, one reference scratch per thread)."""
+    R = ref()
+    luma = np.ascontiguousarray(luma, dtype=np.float64)
+    h = luma.shape[0] if h is None else h
+    w = luma.shape[1]
+    y1 = h if y1 is None else y1
+    out = np.empty((y1 - y0, w), np.float32)
+    rc = R.ref_energy_map_luma_rows(_ptr(luma, _f64p), w, h, n, edges, textures, y0, y1,
+                                    nthreads, _ptr(out, _f32p))
     if rc != 0:
         raise ValueError("reference rejected the call")
     return out

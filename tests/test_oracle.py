@@ -27,7 +27,7 @@ def test_oracle_matches_kat():
 
 
 def test_kat_semantics():
-    """Known answers that follow from src/dct.c:112-126 directly."""
+    """Known answers that follow from src/dct.c:96-110 directly."""
     for n in (2, 4, 8, 16):
         assert O.window_energy(np.full((n, n), 0.42), 0.3, 0.7) == 0.0
         # a pure (0,1) atom -> edge class
