@@ -221,6 +221,7 @@ dcte::FixParams fix_params(const uint8_t* px, long long rowstride, int w, int h,
     q.fix_cap = (unsigned)f->cap;
     q.fix_total = f->d_count + 1;
     q.pts = nullptr;
+    q.max_items = (unsigned)f->cap;
     return q;
 }
 
@@ -272,6 +273,7 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
 
     dcte::FixParams q = fix_params(p.px, rowstride, w, h, in_row0, bpp, n, y0, sem, d_out,
                                    out_stride, edges, textures, f);
+    q.max_items = (unsigned)npix;
 
     DCTE_HIP(ctx, hipMemsetAsync(f->d_count, 0, sizeof(unsigned), s));
     if (ctx->profile) {
@@ -672,6 +674,7 @@ int dcte_energy_points_device(dcte_ctx* ctx, int device, const void* d_px, long 
         dcte::FixParams q = fix_params(p.px, rowstride, w, h, 0, bpp, n, 0, semantics, d_out, 0,
                                        edges, textures, f);
         q.pts = d_xy;
+        q.max_items = (unsigned)count;
         DCTE_HIP(ctx, dcte::launch_fix(q, s));
     }
     return DCTE_OK;

@@ -44,6 +44,7 @@ struct FixParams {
     unsigned fix_cap;
     unsigned* fix_total;     // += pixels refined (host-path diagnostic), or null
     const int* pts;          // points mode: entry k is point k = (pts[2k], pts[2k+1]) -> out[k]
+    unsigned max_items;      // most entries the list can hold for this launch (grid size)
 };
 
 // Seam removal + energy update (dcte_seam.hip) and energies at points.

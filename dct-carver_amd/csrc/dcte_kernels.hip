@@ -365,101 +365,168 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
 }
 
 // ------------------------------------------------------------------ refinement
-// One wave per flagged pixel: the N*N window is gathered in parallel (one
-// element per lane), each 1-D pass of the reference transform runs on N lanes
-// (one lane per line, the reference's own operation sequence, fp64, in LDS),
-// and the last-maximum scan of src/dct.c:100-108 becomes an exact reduction:
-// M = max |C| over the non-DC coefficients, and the winner is the LARGEST
-// linear index k1*N + k2 with |C| == M (that is what "max <= currval" keeps).
-constexpr int kFixWaves = 4;
+// Flagged pixels (and points-mode entries) are recomputed in fp64 in the
+// reference's own operation order (dcte_ref64.h): liblqr luma, the window
+// gather of src/render.c:146-152 (data[dx][dy]; preview data[dy][dx],
+// src/render.c:49), ddct8x8s / ddct16x16s / ddct2d, and the last-maximum scan
+// of src/dct.c:100-108 -- identical class AND value to the reference.
+//
+// Tie-dense frames (line art, isolated dots: exact edge/texture ties in real
+// arithmetic, decided only by the reference's rounding) flag a few % of all
+// pixels, so this is a throughput kernel, not a cleanup pass:
+//  * N <= 8: one LANE per pixel, the whole window in registers (N = 8: 64
+//    doubles), the transform and the scan fully unrolled;
+//  * N = 16: one 16-lane group per pixel (4 pixels per wave) -- 256 doubles do
+//    not fit a lane's registers -- with the window in LDS: each lane gathers 16
+//    elements, runs one line of each pass, scans one coefficient row, and the
+//    group reduces (max, last index) with shuffles.
+// liblqr luma divides each channel by 255 in double; the 256 quotients are
+// tabulated in LDS once per workgroup (bit-identical to dividing).
+constexpr int kFixThreads = 256;
+
+struct Pix {
+    int x, y;
+    long long o;   // output element
+};
+
+__device__ __forceinline__ Pix fix_pixel(const FixParams& p, unsigned k)
+{
+    const unsigned idx = p.fix_list[k];
+    Pix r;
+    if (p.pts) {                                   // points mode
+        r.x = clampi(p.pts[2 * idx], 0, p.w - 1);
+        r.y = clampi(p.pts[2 * idx + 1], 0, p.h - 1);
+        r.o = idx;
+    } else {
+        r.y = p.y0 + (int)(idx / (unsigned)p.w);
+        r.x = (int)(idx % (unsigned)p.w);
+        r.o = (long long)(r.y - p.y0) * p.out_stride + r.x;
+    }
+    return r;
+}
+
+// window element (i, j) of pixel q: liblqr data[dx][dy] (i = column offset),
+// preview data[dy][dx]
+template <int N, int SEM>
+__device__ __forceinline__ double fix_elem(const FixParams& p, const double* lut, const Pix& q,
+                                           int i, int j)
+{
+    constexpr int HL = Geo<N, SEM>::HL;
+    const int ox = SEM == kSemLqr ? i : j, oy = SEM == kSemLqr ? j : i;
+    const int xx = clampi(q.x + ox - HL, 0, p.w - 1);
+    const int yy = clampi(q.y + oy - HL, 0, p.h - 1);
+    const uint8_t* px = p.px + (long long)(yy - p.in_row0) * p.rowstride + (long long)xx * p.bpp;
+    if constexpr (SEM == kSemLqr) {
+        if (p.bpp == 1) return lut[px[0]];
+        return 0.2126 * lut[px[0]] + 0.7152 * lut[px[1]] + 0.0722 * lut[px[2]];
+    } else {
+        return (double)preview_luma(px[0], p.bpp > 1 ? px[1] : 0u, p.bpp > 1 ? px[2] : 0u, p.bpp);
+    }
+}
+
+__device__ __forceinline__ void fix_store(const FixParams& p, const Pix& q, double m, bool edge)
+{
+    p.out[q.o] = edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
+}
 
 template <int N, int SEM>
-__global__ __launch_bounds__(64 * kFixWaves) void dcte_fix(const FixParams p)
+__global__ __launch_bounds__(kFixThreads) void dcte_fix(const FixParams p)
 {
-    __shared__ double win[kFixWaves][N * N];
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    double* d = win[wv];
+    __shared__ double lut[256];
+    constexpr int LDS_PIX = N == 16 ? kFixThreads / 16 : 1;
+    __shared__ double win[LDS_PIX][N == 16 ? 256 : 1];
     const unsigned cnt = min(*p.fix_count, p.fix_cap);
-    constexpr int HL = Geo<N, SEM>::HL;
     if (p.fix_total && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(p.fix_total, cnt);
-    for (unsigned k = blockIdx.x * kFixWaves + wv; k < cnt; k += gridDim.x * kFixWaves) {
-        const unsigned idx = p.fix_list[k];
-        int x, y;
-        long long o;                                   // output element
-        if (p.pts) {                                   // points mode
-            x = clampi(p.pts[2 * idx], 0, p.w - 1);
-            y = clampi(p.pts[2 * idx + 1], 0, p.h - 1);
-            o = idx;
-        } else {
-            y = p.y0 + (int)(idx / (unsigned)p.w);
-            x = (int)(idx % (unsigned)p.w);
-            o = (long long)(y - p.y0) * p.out_stride + x;
+    if (blockIdx.x * (unsigned)(kFixThreads / (N == 16 ? 16 : 1)) >= cnt) return;   // uniform
+    lut[threadIdx.x] = (double)threadIdx.x / 255;
+    __syncthreads();
+
+    if constexpr (N <= 8) {
+        for (unsigned k = blockIdx.x * kFixThreads + threadIdx.x; k < cnt; k += gridDim.x * kFixThreads) {
+            const Pix q = fix_pixel(p, k);
+            double d[N * N];
+#pragma unroll
+            for (int i = 0; i < N; i++)
+#pragma unroll
+                for (int j = 0; j < N; j++) d[i * N + j] = fix_elem<N, SEM>(p, lut, q, i, j);
+            if constexpr (N == 8) {
+                // ddct8x8s: along the first index, then the second
+#pragma unroll
+                for (int i = 0; i < 8; i++) r64::step8(d + i, 8);
+#pragma unroll
+                for (int i = 0; i < 8; i++) r64::step8(d + 8 * i, 1);
+            } else {
+                // ddct2d: the second index first, then the first
+#pragma unroll
+                for (int i = 0; i < N; i++) r64::step_small(N, d + N * i, 1, p.ct);
+#pragma unroll
+                for (int i = 0; i < N; i++) r64::step_small(N, d + i, N, p.ct);
+            }
+            // last maximum (src/dct.c:103: "max <= currval"); the edge atoms
+            // are (0,1) and (1,0) (src/dct.c:18-25)
+            double m = 0.0;
+            bool edge = false;
+#pragma unroll
+            for (int e = 1; e < N * N; e++) {
+                const double v = fabs(d[e]);
+                const bool take = m <= v;
+                m = take ? v : m;
+                edge = take ? (e == 1 || e == N) : edge;
+            }
+            fix_store(p, q, m, edge);
         }
-        for (int e = lane; e < N * N; e += 64) {
-            // liblqr callback: data[dx][dy] (src/render.c:150);
-            // preview: data[dy][dx] (src/render.c:49)
-            const int i = e / N, j = e % N;
-            const int ox = SEM == kSemLqr ? i : j, oy = SEM == kSemLqr ? j : i;
-            const int xx = clampi(x + ox - HL, 0, p.w - 1);
-            const int yy = clampi(y + oy - HL, 0, p.h - 1);
-            const uint8_t* px = p.px + (long long)(yy - p.in_row0) * p.rowstride + (long long)xx * p.bpp;
-            if constexpr (SEM == kSemLqr)
-                d[e] = r64::luma(px, p.bpp);
-            else
-                d[e] = (double)preview_luma(px[0], p.bpp > 1 ? px[1] : 0u, p.bpp > 1 ? px[2] : 0u, p.bpp);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if constexpr (N == 8 || N == 16) {
-            // ddct8x8s / ddct16x16s: along the first index, then the second
-            if (lane < N) {
-                if constexpr (N == 8) r64::step8(d + lane, N); else r64::step16(d + lane, N);
+    } else {
+        // 16 lanes per pixel, 4 pixels per wave; every lane runs every wave
+        // barrier (invalid groups compute on stale LDS and store nothing)
+        const int lane = threadIdx.x & 63, l = lane & 15;
+        const int slot = threadIdx.x >> 4;                        // pixel slot in the block
+        double* d = win[slot];
+        const unsigned per_pass = gridDim.x * (kFixThreads / 16);
+        const unsigned rounds = (cnt + per_pass - 1) / per_pass;   // uniform
+        for (unsigned r = 0; r < rounds; r++) {
+            const unsigned k = r * per_pass + blockIdx.x * (kFixThreads / 16) + slot;
+            const bool valid = k < cnt;
+            Pix q{};
+            if (valid) {
+                q = fix_pixel(p, k);
+#pragma unroll
+                for (int t = 0; t < 16; t++) d[t * 16 + l] = fix_elem<16, SEM>(p, lut, q, t, l);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (lane < N) {
-                if constexpr (N == 8) r64::step8(d + N * lane, 1); else r64::step16(d + N * lane, 1);
-            }
-        } else {
-            // ddct2d: rows (second index) first, then columns
-            if (lane < N) r64::step_small(N, d + N * lane, 1, p.ct);
+            r64::step16(d + l, 16);                  // ddct16x16s: first index ...
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (lane < N) r64::step_small(N, d + lane, N, p.ct);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // exact last-maximum reduction
-        double best = -1.0;
-        int bi = -1;
-        for (int e = lane; e < N * N; e += 64) {
-            if (e == 0) continue;                     // DC (k1 || k2)
-            double v = fabs(d[e]);
-            if (v >= best) {                          // later e wins ties
-                best = v;
-                bi = e;
+            r64::step16(d + 16 * l, 1);              // ... then the second
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // row k1 = l: its last maximum, then the group's (largest index wins ties)
+            double best = -1.0;
+            int bi = -1;
+#pragma unroll
+            for (int c = 0; c < 16; c++) {
+                const int e = l * 16 + c;
+                const double v = fabs(d[e]);
+                const bool take = e != 0 && v >= best;
+                best = take ? v : best;
+                bi = take ? e : bi;
             }
-        }
-        for (int o = 32; o > 0; o >>= 1) {
-            double ob = __shfl_xor(best, o);
-            int oi = __shfl_xor(bi, o);
-            if (ob > best || (ob == best && oi > bi)) {
-                best = ob;
-                bi = oi;
+#pragma unroll
+            for (int o = 8; o > 0; o >>= 1) {
+                const double ob = __shfl_xor(best, o, 16);
+                const int oi = __shfl_xor(bi, o, 16);
+                const bool take = ob > best || (ob == best && oi > bi);
+                best = take ? ob : best;
+                bi = take ? oi : bi;
             }
+            if (valid && l == 0) fix_store(p, q, best, bi == 1 || bi == 16);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        if (lane == 0) {
-            const int k1 = bi / N, k2 = bi % N;
-            const bool edge = (k1 == 0 && k2 == 1) || (k1 == 1 && k2 == 0);
-            p.out[o] = edge ? (float)(best * (double)p.edges) : (float)(best * (double)p.textures);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 
@@ -505,11 +572,15 @@ hipError_t launch_map(int n, int bpp, int sem, const MapParams& p, hipStream_t s
 template <int N>
 static void launch_fix_n(const FixParams& p, hipStream_t s)
 {
-    dim3 grid(256), block(64 * kFixWaves);
+    // enough blocks for the most pixels this launch can flag, capped at ~8
+    // waves per CU; blocks past the device-side count return at once
+    const unsigned per_block = kFixThreads / (N == 16 ? 16 : 1);
+    unsigned blocks = (p.max_items + per_block - 1) / per_block;
+    blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
     if (p.sem == kSemLqr)
-        hipLaunchKernelGGL((dcte_fix<N, kSemLqr>), grid, block, 0, s, p);
+        hipLaunchKernelGGL((dcte_fix<N, kSemLqr>), dim3(blocks), dim3(kFixThreads), 0, s, p);
     else
-        hipLaunchKernelGGL((dcte_fix<N, kSemPreview>), grid, block, 0, s, p);
+        hipLaunchKernelGGL((dcte_fix<N, kSemPreview>), dim3(blocks), dim3(kFixThreads), 0, s, p);
 }
 
 hipError_t launch_fix(const FixParams& p, hipStream_t s)

@@ -26,8 +26,34 @@ def lib():
                                      ctypes.c_size_t, ctypes.c_int, ctypes.c_float,
                                      ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      _f32p, _f32p, _f32p]
+        L.emu_tau_search.restype = ctypes.c_double
+        L.emu_tau_search.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_ulonglong, _u8p,
+                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+        L.emu_window_delta.restype = ctypes.c_double
+        L.emu_window_delta.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p,
+                                       ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         _lib = L
     return _lib
+
+
+def tau_search(n, sem=0, bpp=3, restarts=32, iters=2000, seed=1):
+    """Adversarial search (tests/emu/tau_search.cpp) -> (delta, window, me, mt):
+    the largest fp32 error of a candidate maximum, relative to the window's
+    max coefficient, that the search found."""
+    win = np.zeros((n, n, bpp) if bpp > 1 else (n, n), np.uint8)
+    me, mt = ctypes.c_double(), ctypes.c_double()
+    d = lib().emu_tau_search(n, sem, bpp, restarts, iters, seed, win.ctypes.data_as(_u8p),
+                             ctypes.byref(me), ctypes.byref(mt))
+    return d, win, me.value, mt.value
+
+
+def window_delta(n, win, sem=0):
+    win = np.ascontiguousarray(win, dtype=np.uint8)
+    bpp = 1 if win.ndim == 2 else win.shape[2]
+    me, mt = ctypes.c_double(), ctypes.c_double()
+    d = lib().emu_window_delta(n, sem, bpp, win.ctypes.data_as(_u8p), ctypes.byref(me), ctypes.byref(mt))
+    return d, me.value, mt.value
 
 
 def scale(n, sem=0):

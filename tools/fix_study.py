@@ -1,0 +1,96 @@
+"""Worst-case study of the fp64 tie refinement (dcte_fix) on tie-dense frames.
+
+    python tools/fix_study.py [--size 16384] [--n 8] [--iters 10]
+
+For each frame kind: the number of pixels the map kernel flags (e != t, so
+the class matters), and the device time of the map launch alone (refinement
+off, tie_tau = 0) vs map + refinement (default tau), HIP events on the launch
+stream.  One JSON line per frame.  Line art and isolated dots on flat ground
+hold exact edge/texture ties in real arithmetic (decided only by the
+reference's rounding, src/dct.c:100-108), so they are the worst realistic
+inputs for the refinement.
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "dct-carver_amd")]
+
+
+def frames(S, torch, dev):
+    from dctenergy import synth
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    yy = torch.arange(S, device=dev).view(-1, 1)
+    xx = torch.arange(S, device=dev).view(1, -1)
+    line = ((yy % 23 == 0) | (xx % 31 == 0) | ((xx + 2 * yy) % 97 == 0))
+    grid8 = (yy % 8 == 0) | (xx % 8 == 0)
+    white = lambda m: torch.where(m, 0, 255).to(torch.uint8)
+    rgb = lambda t: t.unsqueeze(-1).expand(S, S, 3).contiguous()
+    dots = torch.rand((S, S), generator=g, device=dev) < 1 / 64
+    text = (torch.rand((S // 4, S // 4), generator=g, device=dev) < 0.3)
+    text = text.repeat_interleave(4, 0).repeat_interleave(4, 1)
+    return {
+        "natural_rgb (bench frame)": synth.natural_rows(0, S, S, 3, seed=0, device=dev),
+        "uniform_rgb": torch.randint(0, 256, (S, S, 3), generator=g, device=dev, dtype=torch.uint8),
+        "lineart_grey": white(line),
+        "lineart_rgb": rgb(white(line)),
+        "grid8_grey": white(grid8),
+        "dots64_grey": torch.where(dots, 255, 16).to(torch.uint8),
+        "text4_grey": white(text),
+        "checker_grey": ((xx + yy) % 2 * 255).to(torch.uint8).expand(S, S).contiguous(),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=16384)
+    ap.add_argument("--n", type=int, default=8)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--edges", type=float, default=0.3)
+    ap.add_argument("--textures", type=float, default=0.7)
+    ap.add_argument("--lib", default=None, help="libdctenergy_hip.so to load (A/B)")
+    a = ap.parse_args()
+    if a.lib:
+        os.environ["DCTE_LIB"] = os.path.abspath(a.lib)
+    import torch
+    import dctenergy
+    dev = torch.device("cuda", 0)
+    S, n, e, t = a.size, a.n, a.edges, a.textures
+    out = torch.empty((S, S), dtype=torch.float32, device=dev)
+    with dctenergy.Context(ngpus=1) as ctx:
+        for name, fr in frames(S, torch, dev).items():
+            stream = torch.cuda.current_stream(dev)
+
+            def timed(tau):
+                ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, tau)
+                ctx.energy_map_tensor(fr, out, n, e, t)        # warm
+                a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a0.record(stream)
+                for _ in range(a.iters):
+                    ctx.energy_map_tensor(fr, out, n, e, t)
+                a1.record(stream)
+                torch.cuda.synchronize()
+                return a0.elapsed_time(a1) / a.iters
+
+            ms_map = timed(0.0)
+            ms_all = timed(4e-6)
+            ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, 4e-6)
+            # flagged count: the host entry point reports it (same kernels)
+            host = fr.cpu().numpy()
+            ctx.energy_map(host, n, e, t)
+            flagged = ctx.last_refined
+            del host
+            res = {"frame": name, "size": S, "n": n, "lib": os.path.basename(dctenergy.LIB_PATH),
+                   "flagged": flagged,
+                   "flagged_frac": round(flagged / (S * S), 5),
+                   "map_ms": round(ms_map, 4), "map_plus_fix_ms": round(ms_all, 4),
+                   "fix_ms": round(ms_all - ms_map, 4),
+                   "fix_frac_of_map": round((ms_all - ms_map) / ms_map, 4)}
+            print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
