@@ -26,9 +26,11 @@ namespace {
 constexpr double kDefaultTieTau = 4e-6;
 
 struct FixScratch {
-    unsigned* d_count = nullptr;   // pixels flagged for refinement
-    unsigned* d_list = nullptr;
+    unsigned* d_count = nullptr;   // [0] list length (points / seam) or dirty tiles (map), [1] refined
+    unsigned* d_list = nullptr;    // flagged pixels (map: per-tile regions)
     size_t cap = 0;
+    unsigned* d_tiles = nullptr;   // map: per-tile counts | dirty-tile list
+    size_t tcap = 0;               // tiles
 };
 
 struct DpScratch {                 // seam DP (dcte_dp.hip), per stream
@@ -173,6 +175,17 @@ int ensure_fix(dcte_ctx* ctx, Device& d, hipStream_t s, size_t npix, FixScratch*
     return DCTE_OK;
 }
 
+int ensure_tiles(dcte_ctx* ctx, FixScratch* f, size_t ntiles)
+{
+    if (f->tcap >= ntiles) return DCTE_OK;
+    if (f->d_tiles) DCTE_HIP(ctx, hipFree(f->d_tiles));
+    f->d_tiles = nullptr;
+    f->tcap = 0;
+    DCTE_HIP(ctx, hipMalloc(&f->d_tiles, 2 * ntiles * sizeof(unsigned)));
+    f->tcap = ntiles;
+    return DCTE_OK;
+}
+
 // the reference's makect (src/fft2d/fftsg.c:724-740) for nc = n, with libm,
 // exactly as the reference evaluates it; used by the fp64 refinement
 void small_twiddles(int n, double ct[4])
@@ -245,8 +258,15 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     if ((long long)dcte::map_default_tile_h(n) * out_stride * 4 >= (1LL << 31)) return DCTE_ERANGE;
 
     DCTE_HIP(ctx, hipSetDevice(d.id));
+    // refinement lists: one region of TW * tile_h entries per map tile
+    const int tiles_x = dcte::map_tiles_x(n, w), tiles_y = dcte::map_tiles_y(n, y1 - y0);
+    const size_t ntiles = (size_t)tiles_x * (size_t)tiles_y;
+    const size_t list_len = ntiles * (size_t)dcte::map_tile_w(n) * (size_t)dcte::map_default_tile_h(n);
+    if (list_len >= (1ULL << 32)) return DCTE_ERANGE;
     FixScratch* f = nullptr;
-    int rc = ensure_fix(ctx, d, s, npix, &f);
+    int rc = ensure_fix(ctx, d, s, list_len, &f);
+    if (rc) return rc;
+    rc = ensure_tiles(ctx, f, ntiles);
     if (rc) return rc;
 
     const double scale = weight_scale(n, sem);
@@ -267,13 +287,16 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     p.tie_tau = (float)ctx->tie_tau;
     p.edges = edges;
     p.textures = textures;
-    p.fix_count = f->d_count;
     p.fix_list = f->d_list;
-    p.fix_cap = (unsigned)f->cap;
+    p.tile_count = f->d_tiles;
+    p.dirty_list = f->d_tiles + ntiles;
+    p.dirty_count = f->d_count;
 
-    dcte::FixParams q = fix_params(p.px, rowstride, w, h, in_row0, bpp, n, y0, sem, d_out,
-                                   out_stride, edges, textures, f);
-    q.max_items = (unsigned)npix;
+    dcte::TileFixParams q{};
+    q.m = p;
+    small_twiddles(n, q.ct);
+    q.fix_total = f->d_count + 1;
+    q.tiles_x = tiles_x;
 
     DCTE_HIP(ctx, hipMemsetAsync(f->d_count, 0, sizeof(unsigned), s));
     if (ctx->profile) {
@@ -288,7 +311,7 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
         DCTE_HIP(ctx, dcte::launch_map(n, bpp, sem, p, s));
     }
     if ((p.we != p.wt && ctx->tie_tau > 0) || ctx->tie_tau >= 1.0)
-        DCTE_HIP(ctx, dcte::launch_fix(q, s));
+        DCTE_HIP(ctx, dcte::launch_fix_tiles(n, bpp, sem, q, s));
     return DCTE_OK;
 }
 
@@ -520,6 +543,7 @@ void dcte_destroy(dcte_ctx* ctx)
             (void)hipStreamSynchronize(kv.first);
             if (kv.second.d_count) (void)hipFree(kv.second.d_count);
             if (kv.second.d_list) (void)hipFree(kv.second.d_list);
+            if (kv.second.d_tiles) (void)hipFree(kv.second.d_tiles);
         }
         for (auto& kv : d.dp) {
             (void)hipStreamSynchronize(kv.first);

@@ -25,9 +25,22 @@ struct MapParams {
     float we, wt;            // edges / textures weights, pre-scaled to luma units
     float tie_tau;           // relative edge/texture margin sent to refinement
     float edges, textures;   // raw weights (refinement path)
-    unsigned* fix_count;     // refinement list (pixel = (y - y0) * w + x)
+    // Refinement lists, per tile (workgroup) t = by * tiles_x + bx: the pixels
+    // it flags, as (y - ys) * TW + (x - x0), at fix_list[t * TW * tile_h ...];
+    // their number in tile_count[t]; the tiles with any in dirty_list[0 ..
+    // *dirty_count) (dcte_fix_tiles walks those).
     unsigned* fix_list;
-    unsigned fix_cap;
+    unsigned* tile_count;
+    unsigned* dirty_list;
+    unsigned* dirty_count;
+};
+
+// dcte_fix_tiles: the map launch's own parameters plus the fp64 pieces
+struct TileFixParams {
+    MapParams m;
+    double ct[4];            // makect twiddles (N = 2, 4)
+    unsigned* fix_total;     // += pixels refined (host-path diagnostic), or null
+    int tiles_x;             // map grid width in tiles
 };
 
 struct FixParams {
@@ -89,6 +102,7 @@ struct DpParams {
 // host-side launchers (dcte_kernels.hip)
 hipError_t launch_map(int n, int bpp, int sem, const MapParams& p, hipStream_t s);
 hipError_t launch_fix(const FixParams& p, hipStream_t s);
+hipError_t launch_fix_tiles(int n, int bpp, int sem, const TileFixParams& p, hipStream_t s);
 hipError_t launch_seam_carve(const SeamParams& p, hipStream_t s);
 hipError_t launch_points(const SeamParams& p, hipStream_t s);
 hipError_t launch_seam_find(const DpParams& p, hipStream_t s);
@@ -100,5 +114,7 @@ int dp_max_tiles(int device);
 // geometry the launcher uses (exported for tests / bench)
 int map_tile_w(int n);
 int map_default_tile_h(int n);
+int map_tiles_x(int n, int w);                 // map grid (tiles) of a launch
+int map_tiles_y(int n, int rows);
 
 }  // namespace dcte

@@ -135,6 +135,7 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
     // waves owning k1 = 0 (q = 0) and k1 = 1 (q = 2) carry an edge candidate
     __shared__ float part_t[S == 4 ? G : 1][S == 4 ? 4 : 1][S == 4 ? 64 : 1];
     __shared__ float part_e[S == 4 ? G : 1][S == 4 ? 2 : 1][S == 4 ? 64 : 1];
+    __shared__ unsigned nflag;                       // pixels this tile flagged
 
     const int tx = threadIdx.x;
     const int lane_p = (S == 4) ? (tx >> 6) : 0;     // N = 16: wave index = k1 class
@@ -209,6 +210,11 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
     __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
         p.out + (long long)(ys - p.y0) * p.out_stride, (short)0,
         (int)((unsigned)(max(ye - ys - 1, 0)) * (unsigned)ostride4 + (unsigned)w * 4u), (int)kBufFlags);
+    // refinement list of this tile (dcte_fix_tiles); nflag is set before the
+    // first barrier and read after the last one
+    const unsigned tile = (unsigned)(by * gridDim.x + bx);
+    unsigned* tile_list = p.fix_list + (size_t)tile * (size_t)(TW * p.tile_h);
+    if (tx == 0) nflag = 0;
     const bool check_ties = we != wt;                // uniform
     const bool force_all = p.tie_tau >= 1.0f;        // uniform
     const float keep = 1.0f - p.tie_tau;             // |me - mt| <= tau * hi  <=>  lo >= (1 - tau) hi
@@ -225,9 +231,10 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
         // error band of hi (never for all-zero windows); every pixel when
         // tie_tau >= 1 (testing)
         if ((check_ties && lo > keep * hi) || force_all) {
-            unsigned k = atomicAdd(p.fix_count, 1u);
-            if (k < p.fix_cap) p.fix_list[k] = (unsigned)((y - p.y0) * w + xx);
-        }    };
+            const unsigned k = atomicAdd(&nflag, 1u);          // < TW * tile_h
+            tile_list[k] = (unsigned)((y - ys) * TW + (xx - x0));
+        }
+    };
 
     // raw dwords of group gg (prefetched in pref) -> raw[b]
     auto stage = [&](int gg, int b) {
@@ -362,6 +369,11 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
             compute(g, 0);
         }
     }
+    __syncthreads();
+    if (tx == 0 && nflag) {
+        p.tile_count[tile] = nflag;
+        p.dirty_list[atomicAdd(p.dirty_count, 1u)] = tile;
+    }
 }
 
 // ------------------------------------------------------------------ refinement
@@ -429,6 +441,73 @@ __device__ __forceinline__ void fix_store(const FixParams& p, const Pix& q, doub
     p.out[q.o] = edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
 }
 
+// The reference transform + last-maximum scan of one window held in
+// registers (N <= 8): ddct8x8s along the first index, then the second;
+// ddct2d (N = 2, 4) the second index first.  The scan keeps the LAST maximum
+// (src/dct.c:103, "max <= currval"); edge atoms (0,1), (1,0) (src/dct.c:18-25).
+template <int N>
+__device__ __forceinline__ void refine_regs(double (&d)[N * N], const double* ct, double& m, bool& edge)
+{
+    if constexpr (N == 8) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) r64::step8(d + i, 8);
+#pragma unroll
+        for (int i = 0; i < 8; i++) r64::step8(d + 8 * i, 1);
+    } else {
+#pragma unroll
+        for (int i = 0; i < N; i++) r64::step_small(N, d + N * i, 1, ct);
+#pragma unroll
+        for (int i = 0; i < N; i++) r64::step_small(N, d + i, N, ct);
+    }
+    m = 0.0;
+    edge = false;
+#pragma unroll
+    for (int e = 1; e < N * N; e++) {
+        const double v = fabs(d[e]);
+        const bool take = m <= v;
+        m = take ? v : m;
+        edge = take ? (e == 1 || e == N) : edge;
+    }
+}
+
+__device__ __forceinline__ void wave_sync_lds()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// N = 16: the 16-lane group of lane l owns the window d[0..255] (LDS, filled
+// and made visible by the caller): ddct16x16s, then row k1 = l's last
+// maximum, then the group's (largest index wins ties).  Every lane of the
+// wave must call it (wave barriers inside).
+__device__ __forceinline__ void refine16_group(double* d, int l, double& best, bool& edge)
+{
+    r64::step16(d + l, 16);                  // along the first index ...
+    wave_sync_lds();
+    r64::step16(d + 16 * l, 1);              // ... then the second
+    wave_sync_lds();
+    best = -1.0;
+    int bi = -1;
+#pragma unroll
+    for (int c = 0; c < 16; c++) {
+        const int e = l * 16 + c;
+        const double v = fabs(d[e]);
+        const bool take = e != 0 && v >= best;
+        best = take ? v : best;
+        bi = take ? e : bi;
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+        const double ob = __shfl_xor(best, o, 16);
+        const int oi = __shfl_xor(bi, o, 16);
+        const bool take = ob > best || (ob == best && oi > bi);
+        best = take ? ob : best;
+        bi = take ? oi : bi;
+    }
+    edge = bi == 1 || bi == 16;
+}
+
 template <int N, int SEM>
 __global__ __launch_bounds__(kFixThreads) void dcte_fix(const FixParams p)
 {
@@ -449,36 +528,15 @@ __global__ __launch_bounds__(kFixThreads) void dcte_fix(const FixParams p)
             for (int i = 0; i < N; i++)
 #pragma unroll
                 for (int j = 0; j < N; j++) d[i * N + j] = fix_elem<N, SEM>(p, lut, q, i, j);
-            if constexpr (N == 8) {
-                // ddct8x8s: along the first index, then the second
-#pragma unroll
-                for (int i = 0; i < 8; i++) r64::step8(d + i, 8);
-#pragma unroll
-                for (int i = 0; i < 8; i++) r64::step8(d + 8 * i, 1);
-            } else {
-                // ddct2d: the second index first, then the first
-#pragma unroll
-                for (int i = 0; i < N; i++) r64::step_small(N, d + N * i, 1, p.ct);
-#pragma unroll
-                for (int i = 0; i < N; i++) r64::step_small(N, d + i, N, p.ct);
-            }
-            // last maximum (src/dct.c:103: "max <= currval"); the edge atoms
-            // are (0,1) and (1,0) (src/dct.c:18-25)
-            double m = 0.0;
-            bool edge = false;
-#pragma unroll
-            for (int e = 1; e < N * N; e++) {
-                const double v = fabs(d[e]);
-                const bool take = m <= v;
-                m = take ? v : m;
-                edge = take ? (e == 1 || e == N) : edge;
-            }
+            double m;
+            bool edge;
+            refine_regs<N>(d, p.ct, m, edge);
             fix_store(p, q, m, edge);
         }
     } else {
         // 16 lanes per pixel, 4 pixels per wave; every lane runs every wave
         // barrier (invalid groups compute on stale LDS and store nothing)
-        const int lane = threadIdx.x & 63, l = lane & 15;
+        const int l = threadIdx.x & 15;
         const int slot = threadIdx.x >> 4;                        // pixel slot in the block
         double* d = win[slot];
         const unsigned per_pass = gridDim.x * (kFixThreads / 16);
@@ -492,47 +550,132 @@ __global__ __launch_bounds__(kFixThreads) void dcte_fix(const FixParams p)
 #pragma unroll
                 for (int t = 0; t < 16; t++) d[t * 16 + l] = fix_elem<16, SEM>(p, lut, q, t, l);
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            r64::step16(d + l, 16);                  // ddct16x16s: first index ...
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            r64::step16(d + 16 * l, 1);              // ... then the second
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // row k1 = l: its last maximum, then the group's (largest index wins ties)
-            double best = -1.0;
-            int bi = -1;
+            wave_sync_lds();
+            double best;
+            bool edge;
+            refine16_group(d, l, best, edge);
+            if (valid && l == 0) fix_store(p, q, best, edge);
+            wave_sync_lds();
+        }
+    }
+}
+
+// Refinement of a map launch, one workgroup per tile with flagged pixels
+// (dcte_map's per-tile lists): the tile's input rows and columns plus the
+// window halo are staged ONCE into LDS as raw bytes, clamped at the frame
+// border (every window element is then a plain LDS read), and the flagged
+// pixels are refined from there -- one lane per pixel for N <= 8, one 16-lane
+// group per pixel for N = 16.  Tie-dense frames (line art, dots on flat
+// ground) flag a few % of all pixels spread over most tiles; reading their
+// windows straight from HBM, one scattered byte per lane, was bound by the
+// texture addresser (17 ms for 7.2 M pixels at 16384^2, profiles/r02).
+template <int N, int SEM>
+struct FixTile {
+    static constexpr int TW = Geo<N, SEM>::TW;
+    static constexpr int TH = N == 16 ? DCTE_TILE_H16 : DCTE_TILE_H;
+    static constexpr int LW = Geo<N, SEM>::LW;
+    static constexpr int R = TH + N - 1;
+};
+
+template <int N, int BPP, int SEM>
+__global__ __launch_bounds__(kFixThreads) void dcte_fix_tiles(const TileFixParams tp)
+{
+    using FT = FixTile<N, SEM>;
+    constexpr int TW = FT::TW, TH = FT::TH, LW = FT::LW, R = FT::R;
+    constexpr int HL = Geo<N, SEM>::HL;
+    constexpr int PB = (LW * BPP + 3) & ~3;            // staged row pitch (bytes)
+    constexpr int NW = N == 16 ? kFixThreads / 16 : 1;
+    __shared__ double lut[256];
+    __shared__ __attribute__((aligned(16))) uint8_t traw[R * PB];
+    __shared__ double win[NW][N == 16 ? 256 : 1];
+    const MapParams& p = tp.m;
+    const unsigned ndirty = *p.dirty_count;
+    if (blockIdx.x >= ndirty) return;                  // uniform
+    const int tx = threadIdx.x;
+    lut[tx] = (double)tx / 255;
+
+    for (unsigned k = blockIdx.x; k < ndirty; k += gridDim.x) {
+        const unsigned tile = p.dirty_list[k];
+        const unsigned cnt = p.tile_count[tile];
+        const int bx = (int)(tile % (unsigned)tp.tiles_x), by = (int)(tile / (unsigned)tp.tiles_x);
+        const int x0 = bx * TW, ys = p.y0 + by * TH, ye = min(ys + TH, p.y1);
+        const int rows = ye - ys + N - 1;
+        if (tp.fix_total && tx == 0) atomicAdd(tp.fix_total, cnt);
+        __syncthreads();                               // the previous tile's reads are done
+        for (int e = tx; e < rows * LW; e += kFixThreads) {
+            const int r = e / LW, c = e - r * LW;
+            const int gy = clampi(ys - HL + r, 0, p.h - 1), gx = clampi(x0 - HL + c, 0, p.w - 1);
+            const uint8_t* src = p.px + (long long)(gy - p.in_row0) * p.rowstride + (long long)gx * BPP;
 #pragma unroll
-            for (int c = 0; c < 16; c++) {
-                const int e = l * 16 + c;
-                const double v = fabs(d[e]);
-                const bool take = e != 0 && v >= best;
-                best = take ? v : best;
-                bi = take ? e : bi;
+            for (int ch = 0; ch < BPP; ch++) traw[r * PB + c * BPP + ch] = src[ch];
+        }
+        __syncthreads();
+        const unsigned* list = p.fix_list + (size_t)tile * (size_t)(TW * TH);
+        // element (i, j) of the window of tile pixel (lx, ly): liblqr
+        // data[dx][dy] (src/render.c:150), preview data[dy][dx] (src/render.c:49)
+        auto elem = [&](int lx, int ly, int i, int j) -> double {
+            const int ox = SEM == kSemLqr ? i : j, oy = SEM == kSemLqr ? j : i;
+            const uint8_t* q = &traw[(ly + oy) * PB + (lx + ox) * BPP];
+            if constexpr (SEM == kSemLqr) {
+                if constexpr (BPP == 1) return lut[q[0]];
+                else return 0.2126 * lut[q[0]] + 0.7152 * lut[q[1]] + 0.0722 * lut[q[2]];
+            } else {
+                return (double)preview_luma(q[0], BPP > 1 ? q[1] : 0u, BPP > 1 ? q[2] : 0u, BPP);
             }
+        };
+        auto store = [&](int lx, int ly, double m, bool edge) {
+            p.out[(long long)(ys + ly - p.y0) * p.out_stride + x0 + lx] =
+                edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
+        };
+        if constexpr (N <= 8) {
+            for (unsigned q = tx; q < cnt; q += kFixThreads) {
+                const unsigned loc = list[q];
+                const int ly = (int)(loc / TW), lx = (int)(loc % TW);
+                double d[N * N];
 #pragma unroll
-            for (int o = 8; o > 0; o >>= 1) {
-                const double ob = __shfl_xor(best, o, 16);
-                const int oi = __shfl_xor(bi, o, 16);
-                const bool take = ob > best || (ob == best && oi > bi);
-                best = take ? ob : best;
-                bi = take ? oi : bi;
+                for (int i = 0; i < N; i++)
+#pragma unroll
+                    for (int j = 0; j < N; j++) d[i * N + j] = elem(lx, ly, i, j);
+                double m;
+                bool edge;
+                refine_regs<N>(d, tp.ct, m, edge);
+                store(lx, ly, m, edge);
             }
-            if (valid && l == 0) fix_store(p, q, best, bi == 1 || bi == 16);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else {
+            const int l = tx & 15, slot = tx >> 4;
+            double* d = win[slot];
+            const unsigned rounds = (cnt + NW - 1) / NW;   // uniform
+            for (unsigned r = 0; r < rounds; r++) {
+                const unsigned q = r * NW + slot;
+                const bool valid = q < cnt;
+                int lx = 0, ly = 0;
+                if (valid) {
+                    const unsigned loc = list[q];
+                    ly = (int)(loc / TW);
+                    lx = (int)(loc % TW);
+#pragma unroll
+                    for (int t = 0; t < 16; t++) d[t * 16 + l] = elem(lx, ly, t, l);
+                }
+                wave_sync_lds();
+                double best;
+                bool edge;
+                refine16_group(d, l, best, edge);
+                if (valid && l == 0) store(lx, ly, best, edge);
+                wave_sync_lds();
+            }
         }
     }
 }
 
 // ------------------------------------------------------------------ launchers
-int map_tile_w(int n) { return n == 16 ? Geo<16, kSemLqr>::TW : Geo<8, kSemLqr>::TW; }
+int map_tile_w(int n)
+{
+    return n == 16 ? Geo<16, kSemLqr>::TW
+                   : (n == 8 ? Geo<8, kSemLqr>::TW : (n == 4 ? Geo<4, kSemLqr>::TW : Geo<2, kSemLqr>::TW));
+}
 int map_default_tile_h(int n) { return n == 16 ? DCTE_TILE_H16 : DCTE_TILE_H; }
+int map_tiles_x(int n, int w) { return (w + map_tile_w(n) - 1) / map_tile_w(n); }
+int map_tiles_y(int n, int rows) { return (rows + map_default_tile_h(n) - 1) / map_default_tile_h(n); }
 
 template <int N, int BPP, int SEM>
 static hipError_t launch_map_t(const MapParams& p, hipStream_t s)
@@ -581,6 +724,43 @@ static void launch_fix_n(const FixParams& p, hipStream_t s)
         hipLaunchKernelGGL((dcte_fix<N, kSemLqr>), dim3(blocks), dim3(kFixThreads), 0, s, p);
     else
         hipLaunchKernelGGL((dcte_fix<N, kSemPreview>), dim3(blocks), dim3(kFixThreads), 0, s, p);
+}
+
+template <int N, int BPP, int SEM>
+static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
+{
+    if (p.m.tile_h != FixTile<N, SEM>::TH || p.tiles_x != (p.m.w + Geo<N, SEM>::TW - 1) / Geo<N, SEM>::TW)
+        return hipErrorInvalidValue;
+    const int ntiles = p.tiles_x * ((p.m.y1 - p.m.y0 + p.m.tile_h - 1) / p.m.tile_h);
+    const int blocks = ntiles < 512 ? ntiles : 512;    // ~1-2 resident per CU (LDS)
+    hipLaunchKernelGGL((dcte_fix_tiles<N, BPP, SEM>), dim3(blocks), dim3(kFixThreads), 0, s, p);
+    return hipGetLastError();
+}
+
+template <int N>
+static hipError_t launch_fix_tiles_n(int bpp, int sem, const TileFixParams& p, hipStream_t s)
+{
+    if (sem == kSemLqr) {
+        if (bpp == 1) return launch_fix_tiles_t<N, 1, kSemLqr>(p, s);
+        if (bpp == 3) return launch_fix_tiles_t<N, 3, kSemLqr>(p, s);
+    } else if (sem == kSemPreview) {
+        if (bpp == 1) return launch_fix_tiles_t<N, 1, kSemPreview>(p, s);
+        if (bpp == 3) return launch_fix_tiles_t<N, 3, kSemPreview>(p, s);
+        if (bpp == 4) return launch_fix_tiles_t<N, 4, kSemPreview>(p, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_fix_tiles(int n, int bpp, int sem, const TileFixParams& p, hipStream_t s)
+{
+    if (p.m.y1 <= p.m.y0) return hipSuccess;
+    switch (n) {
+    case 2: return launch_fix_tiles_n<2>(bpp, sem, p, s);
+    case 4: return launch_fix_tiles_n<4>(bpp, sem, p, s);
+    case 8: return launch_fix_tiles_n<8>(bpp, sem, p, s);
+    case 16: return launch_fix_tiles_n<16>(bpp, sem, p, s);
+    default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_fix(const FixParams& p, hipStream_t s)
