@@ -66,6 +66,9 @@ namespace dcte {
 #ifndef DCTE_PRIO
 #define DCTE_PRIO 1        // wave priority while staging / converting a group (A/B: -2 % at N = 8 and 16)
 #endif
+#ifndef DCTE_FIX_WAVES
+#define DCTE_FIX_WAVES 2   // dcte_fix_tiles: waves per SIMD the register budget allows (2: two tiles per CU)
+#endif
 #ifndef DCTE_XBAL
 #define DCTE_XBAL 1        // halo-column luma conversions spread one per lane of the last wave
 #endif
@@ -561,109 +564,221 @@ __global__ __launch_bounds__(kFixThreads) void dcte_fix(const FixParams p)
 }
 
 // Refinement of a map launch, one workgroup per tile with flagged pixels
-// (dcte_map's per-tile lists): the tile's input rows and columns plus the
-// window halo are staged ONCE into LDS as raw bytes, clamped at the frame
-// border (every window element is then a plain LDS read), and the flagged
-// pixels are refined from there -- one lane per pixel for N <= 8, one 16-lane
-// group per pixel for N = 16.  Tie-dense frames (line art, dots on flat
-// ground) flag a few % of all pixels spread over most tiles; reading their
-// windows straight from HBM, one scattered byte per lane, was bound by the
-// texture addresser (17 ms for 7.2 M pixels at 16384^2, profiles/r02).
+// (dcte_map's per-tile lists).  Tie-dense frames (line art, dots on flat
+// ground) flag a few % of all pixels spread over most tiles; read straight
+// from HBM, one scattered byte per lane, their windows were bound by the
+// texture addresser (17 ms for 7.2 M pixels at 16384^2, profiles/r02).  So:
+//  * a tile with few flagged pixels (cnt <= kFixDirect) gathers its windows
+//    from global memory directly, one lane per pixel -- natural frames flag
+//    ~1 pixel per dirty tile, and staging a whole tile for it would cost more
+//    than the refinement;
+//  * a denser tile is walked in sub-bands of SBH output rows: the sub-band's
+//    input rows (+ window halo, clamped at the frame border) are converted
+//    ONCE to the reference's fp64 luma in LDS, and every window element is
+//    then one 8-byte LDS read.  The map kernel emits its flags in row-group
+//    order (all of group g before group g + 1: the barrier between them), so
+//    sub-bands of whole groups are contiguous ranges of the tile's list
+//    (found with an LDS histogram).
+// One lane per pixel for N <= 8 (the window in registers), one 16-lane group
+// per pixel for N = 16 (the window in LDS).
+constexpr unsigned kFixDirect = 32;
+
 template <int N, int SEM>
 struct FixTile {
     static constexpr int TW = Geo<N, SEM>::TW;
     static constexpr int TH = N == 16 ? DCTE_TILE_H16 : DCTE_TILE_H;
     static constexpr int LW = Geo<N, SEM>::LW;
-    static constexpr int R = TH + N - 1;
+    static constexpr int G = Geo<N, SEM>::G;          // map kernel rows per group
+    static constexpr int GPS = N == 16 ? 3 : (N == 8 ? 3 : 4);   // groups per sub-band
+    static constexpr int SBH = GPS * G;               // output rows per sub-band
+    static constexpr int LR = SBH + N - 1;            // luma rows staged per sub-band
+    static constexpr int NSB = (TH + N - 1 + SBH - 1) / SBH + 1;   // sub-bands per tile (bound)
 };
 
 template <int N, int BPP, int SEM>
-__global__ __launch_bounds__(kFixThreads) void dcte_fix_tiles(const TileFixParams tp)
+__global__ __launch_bounds__(kFixThreads, DCTE_FIX_WAVES) void dcte_fix_tiles(const TileFixParams tp)
 {
     using FT = FixTile<N, SEM>;
-    constexpr int TW = FT::TW, TH = FT::TH, LW = FT::LW, R = FT::R;
+    constexpr int TW = FT::TW, TH = FT::TH, LW = FT::LW, G = FT::G, SBH = FT::SBH, LR = FT::LR;
+    constexpr int NSB = FT::NSB;
     constexpr int HL = Geo<N, SEM>::HL;
-    constexpr int PB = (LW * BPP + 3) & ~3;            // staged row pitch (bytes)
     constexpr int NW = N == 16 ? kFixThreads / 16 : 1;
     __shared__ double lut[256];
-    __shared__ __attribute__((aligned(16))) uint8_t traw[R * PB];
+    __shared__ double lum[LR * LW];                    // fp64 luma of one sub-band (+ halo)
     __shared__ double win[NW][N == 16 ? 256 : 1];
+    __shared__ unsigned sb_n[NSB], sb_off[NSB + 1];
     const MapParams& p = tp.m;
     const unsigned ndirty = *p.dirty_count;
     if (blockIdx.x >= ndirty) return;                  // uniform
     const int tx = threadIdx.x;
     lut[tx] = (double)tx / 255;
+    __syncthreads();
+
+    // liblqr luma of a pixel (src/render.c:315, LQR_ER_LUMA) [liblqr, unverified];
+    // preview: the u8 RGB2LUMINANCE (src/render.h:5)
+    auto luma = [&](const uint8_t* q) -> double {
+        if constexpr (SEM == kSemLqr) {
+            if constexpr (BPP == 1) return lut[q[0]];
+            else return 0.2126 * lut[q[0]] + 0.7152 * lut[q[1]] + 0.0722 * lut[q[2]];
+        } else {
+            return (double)preview_luma(q[0], BPP > 1 ? q[1] : 0u, BPP > 1 ? q[2] : 0u, BPP);
+        }
+    };
+    auto pixel = [&](int gx, int gy) {
+        return p.px + (long long)(gy - p.in_row0) * p.rowstride + (long long)gx * BPP;
+    };
 
     for (unsigned k = blockIdx.x; k < ndirty; k += gridDim.x) {
         const unsigned tile = p.dirty_list[k];
         const unsigned cnt = p.tile_count[tile];
         const int bx = (int)(tile % (unsigned)tp.tiles_x), by = (int)(tile / (unsigned)tp.tiles_x);
         const int x0 = bx * TW, ys = p.y0 + by * TH, ye = min(ys + TH, p.y1);
-        const int rows = ye - ys + N - 1;
-        if (tp.fix_total && tx == 0) atomicAdd(tp.fix_total, cnt);
-        __syncthreads();                               // the previous tile's reads are done
-        for (int e = tx; e < rows * LW; e += kFixThreads) {
-            const int r = e / LW, c = e - r * LW;
-            const int gy = clampi(ys - HL + r, 0, p.h - 1), gx = clampi(x0 - HL + c, 0, p.w - 1);
-            const uint8_t* src = p.px + (long long)(gy - p.in_row0) * p.rowstride + (long long)gx * BPP;
-#pragma unroll
-            for (int ch = 0; ch < BPP; ch++) traw[r * PB + c * BPP + ch] = src[ch];
-        }
-        __syncthreads();
         const unsigned* list = p.fix_list + (size_t)tile * (size_t)(TW * TH);
-        // element (i, j) of the window of tile pixel (lx, ly): liblqr
-        // data[dx][dy] (src/render.c:150), preview data[dy][dx] (src/render.c:49)
-        auto elem = [&](int lx, int ly, int i, int j) -> double {
-            const int ox = SEM == kSemLqr ? i : j, oy = SEM == kSemLqr ? j : i;
-            const uint8_t* q = &traw[(ly + oy) * PB + (lx + ox) * BPP];
-            if constexpr (SEM == kSemLqr) {
-                if constexpr (BPP == 1) return lut[q[0]];
-                else return 0.2126 * lut[q[0]] + 0.7152 * lut[q[1]] + 0.0722 * lut[q[2]];
-            } else {
-                return (double)preview_luma(q[0], BPP > 1 ? q[1] : 0u, BPP > 1 ? q[2] : 0u, BPP);
-            }
-        };
+        if (tp.fix_total && tx == 0) atomicAdd(tp.fix_total, cnt);
         auto store = [&](int lx, int ly, double m, bool edge) {
             p.out[(long long)(ys + ly - p.y0) * p.out_stride + x0 + lx] =
                 edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
         };
-        if constexpr (N <= 8) {
-            for (unsigned q = tx; q < cnt; q += kFixThreads) {
-                const unsigned loc = list[q];
-                const int ly = (int)(loc / TW), lx = (int)(loc % TW);
-                double d[N * N];
+        // window element (i, j) of tile pixel (lx, ly): liblqr data[dx][dy]
+        // (src/render.c:150), preview data[dy][dx] (src/render.c:49)
+        auto offs = [](int i, int j, int& ox, int& oy) {
+            ox = SEM == kSemLqr ? i : j;
+            oy = SEM == kSemLqr ? j : i;
+        };
+
+        if (cnt <= kFixDirect) {
+            // sparse tile: windows straight from global memory
+            if constexpr (N <= 8) {
+                if ((unsigned)tx < cnt) {
+                    const unsigned loc = list[tx];
+                    const int ly = (int)(loc / TW), lx = (int)(loc % TW);
+                    double d[N * N];
 #pragma unroll
-                for (int i = 0; i < N; i++)
+                    for (int i = 0; i < N; i++)
 #pragma unroll
-                    for (int j = 0; j < N; j++) d[i * N + j] = elem(lx, ly, i, j);
-                double m;
-                bool edge;
-                refine_regs<N>(d, tp.ct, m, edge);
-                store(lx, ly, m, edge);
-            }
-        } else {
-            const int l = tx & 15, slot = tx >> 4;
-            double* d = win[slot];
-            const unsigned rounds = (cnt + NW - 1) / NW;   // uniform
-            for (unsigned r = 0; r < rounds; r++) {
-                const unsigned q = r * NW + slot;
-                const bool valid = q < cnt;
-                int lx = 0, ly = 0;
-                if (valid) {
-                    const unsigned loc = list[q];
-                    ly = (int)(loc / TW);
-                    lx = (int)(loc % TW);
-#pragma unroll
-                    for (int t = 0; t < 16; t++) d[t * 16 + l] = elem(lx, ly, t, l);
+                        for (int j = 0; j < N; j++) {
+                            int ox, oy;
+                            offs(i, j, ox, oy);
+                            d[i * N + j] = luma(pixel(clampi(x0 + lx + ox - HL, 0, p.w - 1),
+                                                      clampi(ys + ly + oy - HL, 0, p.h - 1)));
+                        }
+                    double m;
+                    bool edge;
+                    refine_regs<N>(d, tp.ct, m, edge);
+                    store(lx, ly, m, edge);
                 }
-                wave_sync_lds();
-                double best;
-                bool edge;
-                refine16_group(d, l, best, edge);
-                if (valid && l == 0) store(lx, ly, best, edge);
-                wave_sync_lds();
+            } else {
+                const int l = tx & 15, slot = tx >> 4;
+                double* d = win[slot];
+                for (unsigned r0 = 0; r0 < cnt; r0 += NW) {           // uniform
+                    const unsigned q = r0 + slot;
+                    const bool valid = q < cnt;
+                    int lx = 0, ly = 0;
+                    if (valid) {
+                        const unsigned loc = list[q];
+                        ly = (int)(loc / TW);
+                        lx = (int)(loc % TW);
+#pragma unroll
+                        for (int t = 0; t < 16; t++) {
+                            int ox, oy;
+                            offs(t, l, ox, oy);
+                            d[t * 16 + l] = luma(pixel(clampi(x0 + lx + ox - HL, 0, p.w - 1),
+                                                       clampi(ys + ly + oy - HL, 0, p.h - 1)));
+                        }
+                    }
+                    wave_sync_lds();
+                    double best;
+                    bool edge;
+                    refine16_group(d, l, best, edge);
+                    if (valid && l == 0) store(lx, ly, best, edge);
+                    wave_sync_lds();
+                }
+            }
+            continue;
+        }
+
+        // dense tile: sub-band ranges of the list.  Output row ly was emitted
+        // in map group (ly + N - 1) / G; sub-band = group / GPS.
+        if (tx < NSB) sb_n[tx] = 0;
+        __syncthreads();
+        for (unsigned q = tx; q < cnt; q += kFixThreads) {
+            const int ly = (int)(list[q] / TW);
+            atomicAdd(&sb_n[((ly + N - 1) / G) / FT::GPS], 1u);
+        }
+        __syncthreads();
+        if (tx == 0) {
+            unsigned acc = 0;
+            for (int b = 0; b < NSB; b++) {
+                sb_off[b] = acc;
+                acc += sb_n[b];
+            }
+            sb_off[NSB] = acc;
+        }
+        __syncthreads();
+        for (int b = 0; b < NSB; b++) {
+            const unsigned q0 = sb_off[b], q1 = sb_off[b + 1];
+            if (q0 == q1) continue;                    // uniform
+            // output rows of sub-band b: [A, A + SBH); luma rows A - HL ..
+            const int A = b * SBH - (N - 1);
+            const int rows_out = min(A + SBH, ye - ys) - max(A, 0);
+            const int r0 = max(A, 0) - HL;             // first staged row (tile-relative)
+            const int nrows = rows_out + N - 1;
+            __syncthreads();                           // the previous sub-band's reads are done
+            for (int e = tx; e < nrows * LW; e += kFixThreads) {
+                const int r = e / LW, c = e - r * LW;
+                lum[r * LW + c] = luma(pixel(clampi(x0 - HL + c, 0, p.w - 1),
+                                             clampi(ys + r0 + r, 0, p.h - 1)));
+            }
+            __syncthreads();
+            // element (i, j) of pixel (lx, ly): lum row ly + oy - HL - r0, column lx + ox
+            if constexpr (N <= 8) {
+                for (unsigned q = q0 + tx; q < q1; q += kFixThreads) {
+                    const unsigned loc = list[q];
+                    const int ly = (int)(loc / TW), lx = (int)(loc % TW);
+                    const double* base = &lum[(ly - HL - r0) * LW + lx];
+                    double d[N * N];
+#pragma unroll
+                    for (int i = 0; i < N; i++)
+#pragma unroll
+                        for (int j = 0; j < N; j++) {
+                            int ox, oy;
+                            offs(i, j, ox, oy);
+                            d[i * N + j] = base[oy * LW + ox];
+                        }
+                    double m;
+                    bool edge;
+                    refine_regs<N>(d, tp.ct, m, edge);
+                    store(lx, ly, m, edge);
+                }
+            } else {
+                const int l = tx & 15, slot = tx >> 4;
+                double* d = win[slot];
+                for (unsigned rq = q0; rq < q1; rq += NW) {            // uniform
+                    const unsigned q = rq + slot;
+                    const bool valid = q < q1;
+                    int lx = 0, ly = 0;
+                    if (valid) {
+                        const unsigned loc = list[q];
+                        ly = (int)(loc / TW);
+                        lx = (int)(loc % TW);
+                        const double* base = &lum[(ly - HL - r0) * LW + lx];
+#pragma unroll
+                        for (int t = 0; t < 16; t++) {
+                            int ox, oy;
+                            offs(t, l, ox, oy);
+                            d[t * 16 + l] = base[oy * LW + ox];
+                        }
+                    }
+                    wave_sync_lds();
+                    double best;
+                    bool edge;
+                    refine16_group(d, l, best, edge);
+                    if (valid && l == 0) store(lx, ly, best, edge);
+                    wave_sync_lds();
+                }
             }
         }
+        __syncthreads();                               // sb_n / lum reuse by the next tile
     }
 }
 
@@ -732,7 +847,7 @@ static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
     if (p.m.tile_h != FixTile<N, SEM>::TH || p.tiles_x != (p.m.w + Geo<N, SEM>::TW - 1) / Geo<N, SEM>::TW)
         return hipErrorInvalidValue;
     const int ntiles = p.tiles_x * ((p.m.y1 - p.m.y0 + p.m.tile_h - 1) / p.m.tile_h);
-    const int blocks = ntiles < 512 ? ntiles : 512;    // ~1-2 resident per CU (LDS)
+    const int blocks = ntiles < 1024 ? ntiles : 1024;  // 1-2 resident per CU (LDS), 2 rounds
     hipLaunchKernelGGL((dcte_fix_tiles<N, BPP, SEM>), dim3(blocks), dim3(kFixThreads), 0, s, p);
     return hipGetLastError();
 }
