@@ -573,12 +573,13 @@ __global__ __launch_bounds__(kFixThreads) void dcte_fix(const FixParams p)
 //    ~1 pixel per dirty tile, and staging a whole tile for it would cost more
 //    than the refinement;
 //  * a denser tile is walked in sub-bands of SBH output rows: the sub-band's
-//    input rows (+ window halo, clamped at the frame border) are converted
-//    ONCE to the reference's fp64 luma in LDS, and every window element is
-//    then one 8-byte LDS read.  The map kernel emits its flags in row-group
-//    order (all of group g before group g + 1: the barrier between them), so
-//    sub-bands of whole groups are contiguous ranges of the tile's list
-//    (found with an LDS histogram).
+//    input rows (+ window halo) are copied to LDS as raw bytes with coalesced
+//    dword loads (clamped per pixel only in the tiles at the left / right
+//    frame border), converted there ONCE to the reference's fp64 luma, and
+//    every window element is then one 8-byte LDS read.  The map kernel emits
+//    its flags in row-group order (all of group g before group g + 1: the
+//    barrier between them), so sub-bands of whole groups are contiguous
+//    ranges of the tile's list (found with an LDS histogram).
 // One lane per pixel for N <= 8 (the window in registers), one 16-lane group
 // per pixel for N = 16 (the window in LDS).
 constexpr unsigned kFixDirect = 32;
@@ -589,9 +590,9 @@ struct FixTile {
     static constexpr int TH = N == 16 ? DCTE_TILE_H16 : DCTE_TILE_H;
     static constexpr int LW = Geo<N, SEM>::LW;
     static constexpr int G = Geo<N, SEM>::G;          // map kernel rows per group
-    static constexpr int GPS = N == 16 ? 3 : (N == 8 ? 3 : 4);   // groups per sub-band
-    static constexpr int SBH = GPS * G;               // output rows per sub-band
-    static constexpr int LR = SBH + N - 1;            // luma rows staged per sub-band
+    static constexpr int GPS = N == 16 ? 1 : 2;       // groups per sub-band
+    static constexpr int SBH = GPS * G;               // output rows per sub-band (16)
+    static constexpr int LR = SBH + N - 1;            // input rows staged per sub-band
     static constexpr int NSB = (TH + N - 1 + SBH - 1) / SBH + 1;   // sub-bands per tile (bound)
 };
 
@@ -603,8 +604,12 @@ __global__ __launch_bounds__(kFixThreads, DCTE_FIX_WAVES) void dcte_fix_tiles(co
     constexpr int NSB = FT::NSB;
     constexpr int HL = Geo<N, SEM>::HL;
     constexpr int NW = N == 16 ? kFixThreads / 16 : 1;
+    constexpr int PB = ((LW * BPP + 3) & ~3) + 4;      // raw row pitch: the span + misalignment
+    constexpr int PDW = PB / 4;
     __shared__ double lut[256];
     __shared__ double lum[LR * LW];                    // fp64 luma of one sub-band (+ halo)
+    __shared__ __attribute__((aligned(16))) uint32_t raw[LR * PDW];
+    __shared__ unsigned char mis[LR];                  // byte offset of each raw row's first pixel
     __shared__ double win[NW][N == 16 ? 256 : 1];
     __shared__ unsigned sb_n[NSB], sb_off[NSB + 1];
     const MapParams& p = tp.m;
@@ -613,6 +618,14 @@ __global__ __launch_bounds__(kFixThreads, DCTE_FIX_WAVES) void dcte_fix_tiles(co
     const int tx = threadIdx.x;
     lut[tx] = (double)tx / 255;
     __syncthreads();
+
+    // the frame through a bounds-checked buffer resource (as dcte_map)
+    const uintptr_t pbase = reinterpret_cast<uintptr_t>(p.px);
+    const uint32_t base_off = (uint32_t)(pbase & 3u);
+    const unsigned nrec = base_off + (unsigned)((long long)(p.in_rows - 1) * p.rowstride) +
+                          (unsigned)(p.w * BPP);
+    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(pbase - base_off), (short)0, (int)nrec, (int)kBufFlags);
 
     // liblqr luma of a pixel (src/render.c:315, LQR_ER_LUMA) [liblqr, unverified];
     // preview: the u8 RGB2LUMINANCE (src/render.h:5)
@@ -715,19 +728,44 @@ __global__ __launch_bounds__(kFixThreads, DCTE_FIX_WAVES) void dcte_fix_tiles(co
             sb_off[NSB] = acc;
         }
         __syncthreads();
+        // whole rows of the span are contiguous unless the tile touches the
+        // left / right frame border (3 spare bytes: the last dword stays in the row)
+        const bool interior = x0 - HL >= 0 && (x0 - HL + LW) * BPP + 3 <= p.w * BPP;
         for (int b = 0; b < NSB; b++) {
             const unsigned q0 = sb_off[b], q1 = sb_off[b + 1];
             if (q0 == q1) continue;                    // uniform
-            // output rows of sub-band b: [A, A + SBH); luma rows A - HL ..
+            // output rows of sub-band b: [max(A, 0), min(A + SBH, ye - ys)); input
+            // rows from r0 = max(A, 0) - HL (tile-relative)
             const int A = b * SBH - (N - 1);
             const int rows_out = min(A + SBH, ye - ys) - max(A, 0);
-            const int r0 = max(A, 0) - HL;             // first staged row (tile-relative)
+            const int r0 = max(A, 0) - HL;
             const int nrows = rows_out + N - 1;
             __syncthreads();                           // the previous sub-band's reads are done
+            if (interior) {
+                constexpr int SPAN = LW * BPP;
+                for (int e = tx; e < nrows * PDW; e += kFixThreads) {
+                    const int r = e / PDW, dw = e - r * PDW;
+                    const int gy = clampi(ys + r0 + r, 0, p.h - 1);
+                    const uint32_t a = base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
+                                       (uint32_t)((x0 - HL) * BPP);
+                    if (dw == 0) mis[r] = (unsigned char)(a & 3u);
+                    if (dw * 4 < (int)(a & 3u) + SPAN)
+                        raw[r * PDW + dw] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)((a & ~3u) + 4u * dw), 0, 0);
+                }
+            } else {
+                for (int e = tx; e < nrows * LW; e += kFixThreads) {
+                    const int r = e / LW, c = e - r * LW;
+                    const uint8_t* src = pixel(clampi(x0 - HL + c, 0, p.w - 1), clampi(ys + r0 + r, 0, p.h - 1));
+                    uint8_t* dst = reinterpret_cast<uint8_t*>(&raw[r * PDW]) + c * BPP;
+#pragma unroll
+                    for (int ch = 0; ch < BPP; ch++) dst[ch] = src[ch];
+                    if (c == 0) mis[r] = 0;
+                }
+            }
+            __syncthreads();
             for (int e = tx; e < nrows * LW; e += kFixThreads) {
                 const int r = e / LW, c = e - r * LW;
-                lum[r * LW + c] = luma(pixel(clampi(x0 - HL + c, 0, p.w - 1),
-                                             clampi(ys + r0 + r, 0, p.h - 1)));
+                lum[r * LW + c] = luma(reinterpret_cast<const uint8_t*>(&raw[r * PDW]) + mis[r] + c * BPP);
             }
             __syncthreads();
             // element (i, j) of pixel (lx, ly): lum row ly + oy - HL - r0, column lx + ox
@@ -778,7 +816,7 @@ __global__ __launch_bounds__(kFixThreads, DCTE_FIX_WAVES) void dcte_fix_tiles(co
                 }
             }
         }
-        __syncthreads();                               // sb_n / lum reuse by the next tile
+        __syncthreads();                               // sb_n / raw / lum reuse by the next tile
     }
 }
 
