@@ -742,15 +742,28 @@ __global__ __launch_bounds__(kFixThreads, DCTE_FIX_WAVES) void dcte_fix_tiles(co
             const int nrows = rows_out + N - 1;
             __syncthreads();                           // the previous sub-band's reads are done
             if (interior) {
+                // every load of the sub-band in flight at once, then the LDS stores
                 constexpr int SPAN = LW * BPP;
-                for (int e = tx; e < nrows * PDW; e += kFixThreads) {
+                constexpr int U = (LR * PDW + kFixThreads - 1) / kFixThreads;
+                uint32_t v[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int e = tx + u * kFixThreads;
                     const int r = e / PDW, dw = e - r * PDW;
-                    const int gy = clampi(ys + r0 + r, 0, p.h - 1);
-                    const uint32_t a = base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
-                                       (uint32_t)((x0 - HL) * BPP);
-                    if (dw == 0) mis[r] = (unsigned char)(a & 3u);
-                    if (dw * 4 < (int)(a & 3u) + SPAN)
-                        raw[r * PDW + dw] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)((a & ~3u) + 4u * dw), 0, 0);
+                    v[u] = 0;
+                    if (r < nrows) {
+                        const int gy = clampi(ys + r0 + r, 0, p.h - 1);
+                        const uint32_t a = base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
+                                           (uint32_t)((x0 - HL) * BPP);
+                        if (dw == 0) mis[r] = (unsigned char)(a & 3u);
+                        if (dw * 4 < (int)(a & 3u) + SPAN)
+                            v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)((a & ~3u) + 4u * dw), 0, 0);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int e = tx + u * kFixThreads;
+                    if (e < nrows * PDW) raw[e] = v[u];
                 }
             } else {
                 for (int e = tx; e < nrows * LW; e += kFixThreads) {
