@@ -3,8 +3,9 @@
 #
 #   gpurun -- tools/gpu.sh STEP [STEP ...]
 #
-# STEP is NAME or NAME:ARGS (ARGS one quoted word, split on spaces):
-#   tests[:PYTEST-ARGS]    pytest -m gpu (e.g. tests:"-k full_frame")
+# STEP is NAME or NAME:ARGS (ARGS one quoted word, word-split by the shell, so
+# inner quotes group: tests:"-k 'refine or stress'"):
+#   tests[:PYTEST-ARGS]    pytest -m gpu -s (e.g. tests:"-k full_frame")
 #   smoke                  __graft_entry__.smoke()
 #   bench[:ARGS]           python bench.py ARGS          -> NN_bench.json
 #   trace[:ARGS]           rocprofv3 --kernel-trace --stats of bench.py ARGS
@@ -30,14 +31,14 @@ for step in "$@"; do
   echo "== step $tag: $args"
   case "$name" in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
-        -p no:cacheprovider $args > "$OUT/$tag.log" 2>&1
+      eval "timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread \
+        -p no:cacheprovider $args" > "$OUT/$tag.log" 2>&1
       rc=$?; tail -5 "$OUT/$tag.log" ;;
     smoke)
       timeout -k 10 "$T" python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/$tag.log" 2>&1
       rc=$?; tail -2 "$OUT/$tag.log" ;;
     bench)
-      timeout -k 10 "$T" python bench.py $args > "$OUT/$tag.json" 2> "$OUT/$tag.log"
+      eval "timeout -k 10 $T python bench.py $args" > "$OUT/$tag.json" 2> "$OUT/$tag.log"
       rc=$?; cat "$OUT/$tag.json"; [ $rc -eq 0 ] || tail -20 "$OUT/$tag.log" ;;
     trace)
       (cd /tmp && timeout -k 10 "$T" rocprofv3 --kernel-trace --stats -f csv -d "$OUT/$tag" -o run \
@@ -51,7 +52,7 @@ for step in "$@"; do
         -- python3 "$GRAFT_REPO_ROOT/bench.py" $rest > "$OUT/$tag.log" 2>&1)
       rc=$?; tail -3 "$OUT/$tag.log" ;;
     py)
-      timeout -k 10 "$T" python -u $args > "$OUT/$tag.log" 2>&1
+      eval "timeout -k 10 $T python -u $args" > "$OUT/$tag.log" 2>&1
       rc=$?; tail -40 "$OUT/$tag.log" ;;
     *)
       echo "unknown step $name"; exit 2 ;;
