@@ -11,6 +11,8 @@
 #   trace[:ARGS]           rocprofv3 --kernel-trace --stats of bench.py ARGS
 #   pmc:CTRS[:ARGS]        one rocprofv3 --pmc pass, CTRS comma-separated
 #   py:SCRIPT ARGS         python SCRIPT ARGS (tools/kbench.py, tools/*.py)
+#   ptrace:SCRIPT ARGS     rocprofv3 --kernel-trace --stats of python3 SCRIPT ARGS
+#   ppmc:CTRS:SCRIPT ARGS  one rocprofv3 --pmc pass over python3 SCRIPT ARGS
 # Every step runs under its own time limit (STEP_TIMEOUT, default 300 s;
 # tests 900 s) and the script stops at the first failing step: after a fault,
 # an abort or a time limit nothing else touches the GPU.  Output goes to
@@ -50,6 +52,16 @@ for step in "$@"; do
       [ "$args" != "$ctrs" ] && rest=${args#*:}
       (cd /tmp && timeout -k 10 -s KILL 120 rocprofv3 --pmc ${ctrs//,/ } -f csv -d "$OUT/$tag" -o run \
         -- python3 "$GRAFT_REPO_ROOT/bench.py" $rest > "$OUT/$tag.log" 2>&1)
+      rc=$?; tail -3 "$OUT/$tag.log" ;;
+    ptrace)
+      (cd /tmp && eval "timeout -k 10 $T rocprofv3 --kernel-trace --stats -f csv -d $OUT/$tag -o run \
+        -- python3 $GRAFT_REPO_ROOT/$args" > "$OUT/$tag.log" 2>&1)
+      rc=$?; tail -3 "$OUT/$tag.log" ;;
+    ppmc)
+      ctrs=${args%%:*}
+      rest=${args#*:}
+      (cd /tmp && eval "timeout -k 10 -s KILL 120 rocprofv3 --pmc ${ctrs//,/ } -f csv -d $OUT/$tag -o run \
+        -- python3 $GRAFT_REPO_ROOT/$rest" > "$OUT/$tag.log" 2>&1)
       rc=$?; tail -3 "$OUT/$tag.log" ;;
     py)
       eval "timeout -k 10 $T python -u $args" > "$OUT/$tag.log" 2>&1
