@@ -67,7 +67,7 @@ namespace dcte {
 #define DCTE_PRIO 1        // wave priority while staging / converting a group (A/B: -2 % at N = 8 and 16)
 #endif
 #ifndef DCTE_FIX_WAVES
-#define DCTE_FIX_WAVES 2   // dcte_fix_tiles: waves per SIMD the register budget allows (2: two tiles per CU)
+#define DCTE_FIX_WAVES 1   // dcte_fix_tiles: waves per SIMD the register budget allows (2 spills at N = 8)
 #endif
 #ifndef DCTE_XBAL
 #define DCTE_XBAL 1        // halo-column luma conversions spread one per lane of the last wave
@@ -590,8 +590,8 @@ struct FixTile {
     static constexpr int TH = N == 16 ? DCTE_TILE_H16 : DCTE_TILE_H;
     static constexpr int LW = Geo<N, SEM>::LW;
     static constexpr int G = Geo<N, SEM>::G;          // map kernel rows per group
-    static constexpr int GPS = N == 16 ? 1 : 2;       // groups per sub-band
-    static constexpr int SBH = GPS * G;               // output rows per sub-band (16)
+    static constexpr int GPS = N == 16 ? 2 : 5;       // groups per sub-band
+    static constexpr int SBH = GPS * G;               // output rows per sub-band (40; N = 16: 32)
     static constexpr int LR = SBH + N - 1;            // input rows staged per sub-band
     static constexpr int NSB = (TH + N - 1 + SBH - 1) / SBH + 1;   // sub-bands per tile (bound)
 };
@@ -731,39 +731,60 @@ __global__ __launch_bounds__(kFixThreads, DCTE_FIX_WAVES) void dcte_fix_tiles(co
         // whole rows of the span are contiguous unless the tile touches the
         // left / right frame border (3 spare bytes: the last dword stays in the row)
         const bool interior = x0 - HL >= 0 && (x0 - HL + LW) * BPP + 3 <= p.w * BPP;
-        for (int b = 0; b < NSB; b++) {
-            const unsigned q0 = sb_off[b], q1 = sb_off[b + 1];
-            if (q0 == q1) continue;                    // uniform
-            // output rows of sub-band b: [max(A, 0), min(A + SBH, ye - ys)); input
-            // rows from r0 = max(A, 0) - HL (tile-relative)
+        // sub-band b: output rows [max(A, 0), min(A + SBH, ye - ys)), A = b SBH - (N - 1);
+        // input rows from r0 = max(A, 0) - HL (tile-relative)
+        auto band_rows = [&](int b, int& r0, int& nrows) {
             const int A = b * SBH - (N - 1);
-            const int rows_out = min(A + SBH, ye - ys) - max(A, 0);
-            const int r0 = max(A, 0) - HL;
-            const int nrows = rows_out + N - 1;
+            r0 = max(A, 0) - HL;
+            nrows = min(A + SBH, ye - ys) - max(A, 0) + N - 1;
+        };
+        // raw dwords of a sub-band's rows (interior tiles), all loads in flight
+        // at once; they land in registers while the previous sub-band computes
+        constexpr int SPAN = LW * BPP;
+        constexpr int U = (LR * PDW + kFixThreads - 1) / kFixThreads;
+        uint32_t v[U];
+        auto issue = [&](int b) {
+            int r0, nrows;
+            band_rows(b, r0, nrows);
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int e = tx + u * kFixThreads;
+                const int r = e / PDW, dw = e - r * PDW;
+                v[u] = 0;
+                if (r < nrows) {
+                    const int gy = clampi(ys + r0 + r, 0, p.h - 1);
+                    const uint32_t a = base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
+                                       (uint32_t)((x0 - HL) * BPP);
+                    if (dw * 4 < (int)(a & 3u) + SPAN)
+                        v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)((a & ~3u) + 4u * dw), 0, 0);
+                }
+            }
+        };
+        auto next_band = [&](int b) {
+            for (b = b + 1; b < NSB; b++)
+                if (sb_off[b] != sb_off[b + 1]) return b;
+            return NSB;
+        };
+        int b = next_band(-1);
+        if (interior && b < NSB) issue(b);
+        for (; b < NSB; ) {
+            const unsigned q0 = sb_off[b], q1 = sb_off[b + 1];
+            int r0, nrows;
+            band_rows(b, r0, nrows);
             __syncthreads();                           // the previous sub-band's reads are done
             if (interior) {
-                // every load of the sub-band in flight at once, then the LDS stores
-                constexpr int SPAN = LW * BPP;
-                constexpr int U = (LR * PDW + kFixThreads - 1) / kFixThreads;
-                uint32_t v[U];
 #pragma unroll
                 for (int u = 0; u < U; u++) {
                     const int e = tx + u * kFixThreads;
-                    const int r = e / PDW, dw = e - r * PDW;
-                    v[u] = 0;
+                    const int r = e / PDW;
                     if (r < nrows) {
-                        const int gy = clampi(ys + r0 + r, 0, p.h - 1);
-                        const uint32_t a = base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
-                                           (uint32_t)((x0 - HL) * BPP);
-                        if (dw == 0) mis[r] = (unsigned char)(a & 3u);
-                        if (dw * 4 < (int)(a & 3u) + SPAN)
-                            v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)((a & ~3u) + 4u * dw), 0, 0);
+                        raw[e] = v[u];
+                        if (e - r * PDW == 0) {
+                            const int gy = clampi(ys + r0 + r, 0, p.h - 1);
+                            mis[r] = (unsigned char)((base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
+                                                      (uint32_t)((x0 - HL) * BPP)) & 3u);
+                        }
                     }
-                }
-#pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const int e = tx + u * kFixThreads;
-                    if (e < nrows * PDW) raw[e] = v[u];
                 }
             } else {
                 for (int e = tx; e < nrows * LW; e += kFixThreads) {
@@ -780,10 +801,15 @@ __global__ __launch_bounds__(kFixThreads, DCTE_FIX_WAVES) void dcte_fix_tiles(co
                 const int r = e / LW, c = e - r * LW;
                 lum[r * LW + c] = luma(reinterpret_cast<const uint8_t*>(&raw[r * PDW]) + mis[r] + c * BPP);
             }
+            const int bn = next_band(b);
+            if (interior && bn < NSB) issue(bn);       // lands during this sub-band's compute
             __syncthreads();
             // element (i, j) of pixel (lx, ly): lum row ly + oy - HL - r0, column lx + ox
             if constexpr (N <= 8) {
-                for (unsigned q = q0 + tx; q < q1; q += kFixThreads) {
+                // entries dealt round-robin over the four waves (a sub-band
+                // often holds fewer than 256: all SIMDs get a share)
+                const int slot = (tx & 63) * 4 + (tx >> 6);
+                for (unsigned q = q0 + slot; q < q1; q += kFixThreads) {
                     const unsigned loc = list[q];
                     const int ly = (int)(loc / TW), lx = (int)(loc % TW);
                     const double* base = &lum[(ly - HL - r0) * LW + lx];
@@ -802,8 +828,8 @@ __global__ __launch_bounds__(kFixThreads, DCTE_FIX_WAVES) void dcte_fix_tiles(co
                     store(lx, ly, m, edge);
                 }
             } else {
-                const int l = tx & 15, slot = tx >> 4;
-                double* d = win[slot];
+                const int l = tx & 15, slot = (tx >> 4 & 3) * 4 + (tx >> 6);   // groups round-robin over waves
+                double* d = win[tx >> 4];
                 for (unsigned rq = q0; rq < q1; rq += NW) {            // uniform
                     const unsigned q = rq + slot;
                     const bool valid = q < q1;
@@ -828,6 +854,7 @@ __global__ __launch_bounds__(kFixThreads, DCTE_FIX_WAVES) void dcte_fix_tiles(co
                     wave_sync_lds();
                 }
             }
+            b = bn;
         }
         __syncthreads();                               // sb_n / raw / lum reuse by the next tile
     }
