@@ -258,10 +258,10 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     if ((long long)dcte::map_default_tile_h(n) * out_stride * 4 >= (1LL << 31)) return DCTE_ERANGE;
 
     DCTE_HIP(ctx, hipSetDevice(d.id));
-    // refinement lists: one region of TW * tile_h entries per map tile
+    // refinement lists: one region of 64 * tile_h entries per 64-column strip
     const int tiles_x = dcte::map_tiles_x(n, w), tiles_y = dcte::map_tiles_y(n, y1 - y0);
-    const size_t ntiles = (size_t)tiles_x * (size_t)tiles_y;
-    const size_t list_len = ntiles * (size_t)dcte::map_tile_w(n) * (size_t)dcte::map_default_tile_h(n);
+    const size_t ntiles = (size_t)tiles_x * (size_t)tiles_y * (size_t)dcte::map_strips_per_tile(n);
+    const size_t list_len = ntiles * 64 * (size_t)dcte::map_default_tile_h(n);
     if (list_len >= (1ULL << 32)) return DCTE_ERANGE;
     FixScratch* f = nullptr;
     int rc = ensure_fix(ctx, d, s, list_len, &f);

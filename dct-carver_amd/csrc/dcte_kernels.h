@@ -25,17 +25,18 @@ struct MapParams {
     float we, wt;            // edges / textures weights, pre-scaled to luma units
     float tie_tau;           // relative edge/texture margin sent to refinement
     float edges, textures;   // raw weights (refinement path)
-    // Refinement lists, per tile (workgroup) t = by * tiles_x + bx: the pixels
-    // it flags, as (y - ys) * TW + (x - x0), at fix_list[t * TW * tile_h ...];
-    // their number in tile_count[t]; the tiles with any in dirty_list[0 ..
-    // *dirty_count) (dcte_fix_tiles walks those).
+    // Refinement lists, per 64-column strip s = (by * tiles_x + bx) * SPT +
+    // strip in the tile (SPT = TW / 64 at N <= 8, 1 at N = 16): the pixels it
+    // flags, as (y - ys) * 64 + (x - strip x0), at fix_list[s * 64 * tile_h ...];
+    // their number in tile_count[s]; the strips with any in dirty_list[0 ..
+    // *dirty_count) (dcte_fix_strips walks those).
     unsigned* fix_list;
     unsigned* tile_count;
     unsigned* dirty_list;
     unsigned* dirty_count;
 };
 
-// dcte_fix_tiles: the map launch's own parameters plus the fp64 pieces
+// dcte_fix_strips: the map launch's own parameters plus the fp64 pieces
 struct TileFixParams {
     MapParams m;
     double ct[4];            // makect twiddles (N = 2, 4)
@@ -116,5 +117,6 @@ int map_tile_w(int n);
 int map_default_tile_h(int n);
 int map_tiles_x(int n, int w);                 // map grid (tiles) of a launch
 int map_tiles_y(int n, int rows);
+int map_strips_per_tile(int n);
 
 }  // namespace dcte

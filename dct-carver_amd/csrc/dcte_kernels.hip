@@ -66,9 +66,6 @@ namespace dcte {
 #ifndef DCTE_PRIO
 #define DCTE_PRIO 1        // wave priority while staging / converting a group (A/B: -2 % at N = 8 and 16)
 #endif
-#ifndef DCTE_FIX_WAVES
-#define DCTE_FIX_WAVES 1   // dcte_fix_tiles: waves per SIMD the register budget allows (2 spills at N = 8)
-#endif
 #ifndef DCTE_XBAL
 #define DCTE_XBAL 1        // halo-column luma conversions spread one per lane of the last wave
 #endif
@@ -138,7 +135,9 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
     // waves owning k1 = 0 (q = 0) and k1 = 1 (q = 2) carry an edge candidate
     __shared__ float part_t[S == 4 ? G : 1][S == 4 ? 4 : 1][S == 4 ? 64 : 1];
     __shared__ float part_e[S == 4 ? G : 1][S == 4 ? 2 : 1][S == 4 ? 64 : 1];
-    __shared__ unsigned nflag;                       // pixels this tile flagged
+    // refinement lists per 64-column strip (one wave's columns; N = 16: the tile)
+    constexpr int SPT = S == 1 ? TW / 64 : 1;        // strips per tile
+    __shared__ unsigned nflag[SPT];                  // pixels each strip flagged
 
     const int tx = threadIdx.x;
     const int lane_p = (S == 4) ? (tx >> 6) : 0;     // N = 16: wave index = k1 class
@@ -213,11 +212,13 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
     __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
         p.out + (long long)(ys - p.y0) * p.out_stride, (short)0,
         (int)((unsigned)(max(ye - ys - 1, 0)) * (unsigned)ostride4 + (unsigned)w * 4u), (int)kBufFlags);
-    // refinement list of this tile (dcte_fix_tiles); nflag is set before the
-    // first barrier and read after the last one
-    const unsigned tile = (unsigned)(by * gridDim.x + bx);
-    unsigned* tile_list = p.fix_list + (size_t)tile * (size_t)(TW * p.tile_h);
-    if (tx == 0) nflag = 0;
+    // refinement lists of this tile's strips (dcte_fix_strips); nflag is set
+    // before the first barrier and read after the last one
+    const int sc = S == 1 ? c >> 6 : 0;              // this thread's strip in the tile
+    const unsigned strip = (unsigned)(by * gridDim.x + bx) * SPT + sc;
+    unsigned* strip_list = p.fix_list + (size_t)strip * (size_t)(64 * p.tile_h);
+    const int sx0 = x0 + 64 * sc;                    // first column of the strip
+    if (tx < SPT) nflag[tx] = 0;
     const bool check_ties = we != wt;                // uniform
     const bool force_all = p.tie_tau >= 1.0f;        // uniform
     const float keep = 1.0f - p.tie_tau;             // |me - mt| <= tau * hi  <=>  lo >= (1 - tau) hi
@@ -234,8 +235,8 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
         // error band of hi (never for all-zero windows); every pixel when
         // tie_tau >= 1 (testing)
         if ((check_ties && lo > keep * hi) || force_all) {
-            const unsigned k = atomicAdd(&nflag, 1u);          // < TW * tile_h
-            tile_list[k] = (unsigned)((y - ys) * TW + (xx - x0));
+            const unsigned k = atomicAdd(&nflag[sc], 1u);      // < 64 * tile_h
+            strip_list[k] = (unsigned)((y - ys) * 64 + (xx - sx0));
         }
     };
 
@@ -373,9 +374,10 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
         }
     }
     __syncthreads();
-    if (tx == 0 && nflag) {
-        p.tile_count[tile] = nflag;
-        p.dirty_list[atomicAdd(p.dirty_count, 1u)] = tile;
+    if (tx < SPT && nflag[tx]) {
+        const unsigned st = strip - sc + tx;
+        p.tile_count[st] = nflag[tx];
+        p.dirty_list[atomicAdd(p.dirty_count, 1u)] = st;
     }
 }
 
@@ -452,10 +454,18 @@ template <int N>
 __device__ __forceinline__ void refine_regs(double (&d)[N * N], const double* ct, double& m, bool& edge)
 {
     if constexpr (N == 8) {
+        // one 8-point step at a time: interleaving all eight would need their
+        // temporaries live beside the 64-element window (> 256 registers)
 #pragma unroll
-        for (int i = 0; i < 8; i++) r64::step8(d + i, 8);
+        for (int i = 0; i < 8; i++) {
+            r64::step8(d + i, 8);
+            __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
-        for (int i = 0; i < 8; i++) r64::step8(d + 8 * i, 1);
+        for (int i = 0; i < 8; i++) {
+            r64::step8(d + 8 * i, 1);
+            __builtin_amdgcn_sched_barrier(0);
+        }
     } else {
 #pragma unroll
         for (int i = 0; i < N; i++) r64::step_small(N, d + N * i, 1, ct);
@@ -563,61 +573,139 @@ __global__ __launch_bounds__(kFixThreads) void dcte_fix(const FixParams p)
     }
 }
 
-// Refinement of a map launch, one workgroup per tile with flagged pixels
-// (dcte_map's per-tile lists).  Tie-dense frames (line art, dots on flat
-// ground) flag a few % of all pixels spread over most tiles; read straight
-// from HBM, one scattered byte per lane, their windows were bound by the
-// texture addresser (17 ms for 7.2 M pixels at 16384^2, profiles/r02).  So:
-//  * a tile with few flagged pixels (cnt <= kFixDirect) gathers its windows
+// Refinement of a map launch: one wave per 64-column STRIP with flagged
+// pixels (dcte_map keeps a list per strip -- one wave's columns at N <= 8, the
+// whole 64-column tile at N = 16 -- in the row order it emitted them).
+// Tie-dense frames (line art, dots on flat ground) flag a few % of all pixels
+// over most strips; read straight from HBM, one scattered byte per lane,
+// their windows were bound by the texture addresser (17 ms for 7.2 M pixels
+// at 16384^2, profiles/r02).  So each wave works alone (no workgroup
+// barriers; several strips per CU hide each other's latency):
+//  * a strip with few flagged pixels (cnt <= kFixDirect) gathers its windows
 //    from global memory directly, one lane per pixel -- natural frames flag
-//    ~1 pixel per dirty tile, and staging a whole tile for it would cost more
-//    than the refinement;
-//  * a denser tile is walked in sub-bands of SBH output rows: the sub-band's
-//    input rows (+ window halo) are copied to LDS as raw bytes with coalesced
-//    dword loads (clamped per pixel only in the tiles at the left / right
-//    frame border), converted there ONCE to the reference's fp64 luma, and
-//    every window element is then one 8-byte LDS read.  The map kernel emits
-//    its flags in row-group order (all of group g before group g + 1: the
-//    barrier between them), so sub-bands of whole groups are contiguous
-//    ranges of the tile's list (found with an LDS histogram).
+//    ~1 pixel per dirty strip;
+//  * a denser strip is walked in bands of SBH output rows: the band's input
+//    rows + window halo are copied to LDS with coalesced dword loads (clamped
+//    per pixel only in strips at the left / right frame border), converted
+//    there ONCE to the reference's fp64 luma, and every window element is one
+//    8-byte LDS read.  Entries come in row-group order, so the wave steps
+//    through them 64 at a time and stages each band once.
 // One lane per pixel for N <= 8 (the window in registers), one 16-lane group
 // per pixel for N = 16 (the window in LDS).
 constexpr unsigned kFixDirect = 32;
 
 template <int N, int SEM>
-struct FixTile {
-    static constexpr int TW = Geo<N, SEM>::TW;
+struct FixStrip {
     static constexpr int TH = N == 16 ? DCTE_TILE_H16 : DCTE_TILE_H;
-    static constexpr int LW = Geo<N, SEM>::LW;
+    static constexpr int SPT = Lanes<N>::S == 1 ? Geo<N, SEM>::TW / 64 : 1;   // strips per tile
+    static constexpr int LW = 64 + N - 1;             // luma columns of a strip
     static constexpr int G = Geo<N, SEM>::G;          // map kernel rows per group
-    static constexpr int GPS = N == 16 ? 2 : 5;       // groups per sub-band
-    static constexpr int SBH = GPS * G;               // output rows per sub-band (40; N = 16: 32)
-    static constexpr int LR = SBH + N - 1;            // input rows staged per sub-band
-    static constexpr int NSB = (TH + N - 1 + SBH - 1) / SBH + 1;   // sub-bands per tile (bound)
+    static constexpr int GPS = N == 16 ? 1 : 3;       // groups per band
+    static constexpr int SBH = GPS * G;               // output rows per band (24; N = 16: 16)
+    static constexpr int LR = SBH + N - 1;            // input rows staged per band
 };
 
-template <int N, int BPP, int SEM>
-__global__ __launch_bounds__(kFixThreads, DCTE_FIX_WAVES) void dcte_fix_tiles(const TileFixParams tp)
+__device__ __forceinline__ int wave_min(int v)
 {
-    using FT = FixTile<N, SEM>;
-    constexpr int TW = FT::TW, TH = FT::TH, LW = FT::LW, G = FT::G, SBH = FT::SBH, LR = FT::LR;
-    constexpr int NSB = FT::NSB;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+    return v;
+}
+
+// dcte_fix_strips: stage band b of a strip -- its input rows + window halo
+// as raw bytes (coalesced dwords; clamped per pixel at the left / right
+// frame border), then as the reference's fp64 luma -- in this wave's LDS.
+// Returns the band's first input row (tile-relative).  Not inlined: the
+// band is staged a few times per strip, and inlined into the refinement loop
+// its loads-in-flight share registers with the 64-element window.
+template <int N, int BPP, int SEM>
+__device__ __noinline__ int fix_stage_band(const MapParams& p, __amdgpu_buffer_rsrc_t rsrc,
+                                           uint32_t base_off, const double* lut, double* lum,
+                                           uint32_t* raw, unsigned char* mis, int b, int sx0, int ys,
+                                           int ye, bool interior, int lane)
+{
+    using FS = FixStrip<N, SEM>;
+    constexpr int LW = FS::LW, SBH = FS::SBH, LR = FS::LR;
     constexpr int HL = Geo<N, SEM>::HL;
-    constexpr int NW = N == 16 ? kFixThreads / 16 : 1;
+    constexpr int PDW = (((LW * BPP + 3) & ~3) + 4) / 4;
+    const int A = b * SBH - (N - 1);
+    const int r0 = max(A, 0) - HL;
+    const int nrows = min(A + SBH, ye - ys) - max(A, 0) + N - 1;
+    wave_sync_lds();                               // the previous band's reads are done
+    if (interior) {
+        // every load of the band in flight at once, then the LDS stores
+        constexpr int SPAN = LW * BPP;
+        constexpr int U = (LR * PDW + 63) / 64;
+        uint32_t v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int e = lane + 64 * u;
+            const int r = e / PDW, dw = e - r * PDW;
+            v[u] = 0;
+            if (r < nrows) {
+                const int gy = clampi(ys + r0 + r, 0, p.h - 1);
+                const uint32_t a = base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
+                                   (uint32_t)((sx0 - HL) * BPP);
+                if (dw == 0) mis[r] = (unsigned char)(a & 3u);
+                if (dw * 4 < (int)(a & 3u) + SPAN)
+                    v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)((a & ~3u) + 4u * dw), 0, 0);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int e = lane + 64 * u;
+            if (e < nrows * PDW) raw[e] = v[u];
+        }
+    } else {
+        for (int e = lane; e < nrows * LW; e += 64) {
+            const int r = e / LW, c = e - r * LW;
+            const uint8_t* src = p.px + (long long)(clampi(ys + r0 + r, 0, p.h - 1) - p.in_row0) * p.rowstride +
+                                 (long long)clampi(sx0 - HL + c, 0, p.w - 1) * BPP;
+            uint8_t* dst = reinterpret_cast<uint8_t*>(&raw[r * PDW]) + c * BPP;
+#pragma unroll
+            for (int ch = 0; ch < BPP; ch++) dst[ch] = src[ch];
+            if (c == 0) mis[r] = 0;
+        }
+    }
+    wave_sync_lds();
+    for (int e = lane; e < nrows * LW; e += 64) {
+        const int r = e / LW, c = e - r * LW;
+        const uint8_t* q = reinterpret_cast<const uint8_t*>(&raw[r * PDW]) + mis[r] + c * BPP;
+        double L;
+        if constexpr (SEM == kSemLqr) {
+            if constexpr (BPP == 1) L = lut[q[0]];
+            else L = 0.2126 * lut[q[0]] + 0.7152 * lut[q[1]] + 0.0722 * lut[q[2]];
+        } else {
+            L = (double)preview_luma(q[0], BPP > 1 ? q[1] : 0u, BPP > 1 ? q[2] : 0u, BPP);
+        }
+        lum[r * LW + c] = L;
+    }
+    wave_sync_lds();
+    return r0;
+}
+
+template <int N, int BPP, int SEM>
+__global__ __launch_bounds__(64, 2) void dcte_fix_strips(const TileFixParams tp)
+{
+    using FS = FixStrip<N, SEM>;
+    constexpr int TH = FS::TH, SPT = FS::SPT, LW = FS::LW, G = FS::G, SBH = FS::SBH, LR = FS::LR;
+    constexpr int TW = Geo<N, SEM>::TW;
+    constexpr int HL = Geo<N, SEM>::HL;
     constexpr int PB = ((LW * BPP + 3) & ~3) + 4;      // raw row pitch: the span + misalignment
     constexpr int PDW = PB / 4;
+    constexpr int kBig = 1 << 30;
     __shared__ double lut[256];
-    __shared__ double lum[LR * LW];                    // fp64 luma of one sub-band (+ halo)
+    __shared__ double lum[LR * LW];                    // fp64 luma of one band (+ halo)
     __shared__ __attribute__((aligned(16))) uint32_t raw[LR * PDW];
     __shared__ unsigned char mis[LR];                  // byte offset of each raw row's first pixel
-    __shared__ double win[NW][N == 16 ? 256 : 1];
-    __shared__ unsigned sb_n[NSB], sb_off[NSB + 1];
+    __shared__ double win[N == 16 ? 4 : 1][N == 16 ? 256 : 1];
     const MapParams& p = tp.m;
     const unsigned ndirty = *p.dirty_count;
     if (blockIdx.x >= ndirty) return;                  // uniform
-    const int tx = threadIdx.x;
-    lut[tx] = (double)tx / 255;
-    __syncthreads();
+    const int lane = threadIdx.x;
+#pragma unroll
+    for (int t = 0; t < 4; t++) lut[lane + 64 * t] = (double)(lane + 64 * t) / 255;
+    wave_sync_lds();
 
     // the frame through a bounds-checked buffer resource (as dcte_map)
     const uintptr_t pbase = reinterpret_cast<uintptr_t>(p.px);
@@ -640,31 +728,33 @@ __global__ __launch_bounds__(kFixThreads, DCTE_FIX_WAVES) void dcte_fix_tiles(co
     auto pixel = [&](int gx, int gy) {
         return p.px + (long long)(gy - p.in_row0) * p.rowstride + (long long)gx * BPP;
     };
+    // window element (i, j): liblqr data[dx][dy] (src/render.c:150), preview
+    // data[dy][dx] (src/render.c:49)
+    auto offs = [](int i, int j, int& ox, int& oy) {
+        ox = SEM == kSemLqr ? i : j;
+        oy = SEM == kSemLqr ? j : i;
+    };
 
     for (unsigned k = blockIdx.x; k < ndirty; k += gridDim.x) {
-        const unsigned tile = p.dirty_list[k];
-        const unsigned cnt = p.tile_count[tile];
+        const unsigned strip = p.dirty_list[k];
+        const unsigned cnt = p.tile_count[strip];
+        const unsigned tile = strip / SPT;
         const int bx = (int)(tile % (unsigned)tp.tiles_x), by = (int)(tile / (unsigned)tp.tiles_x);
-        const int x0 = bx * TW, ys = p.y0 + by * TH, ye = min(ys + TH, p.y1);
-        const unsigned* list = p.fix_list + (size_t)tile * (size_t)(TW * TH);
-        if (tp.fix_total && tx == 0) atomicAdd(tp.fix_total, cnt);
+        const int sx0 = bx * TW + 64 * (int)(strip % SPT);
+        const int ys = p.y0 + by * TH, ye = min(ys + TH, p.y1);
+        const unsigned* list = p.fix_list + (size_t)strip * (size_t)(64 * TH);
+        if (tp.fix_total && lane == 0) atomicAdd(tp.fix_total, cnt);
         auto store = [&](int lx, int ly, double m, bool edge) {
-            p.out[(long long)(ys + ly - p.y0) * p.out_stride + x0 + lx] =
+            p.out[(long long)(ys + ly - p.y0) * p.out_stride + sx0 + lx] =
                 edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
-        };
-        // window element (i, j) of tile pixel (lx, ly): liblqr data[dx][dy]
-        // (src/render.c:150), preview data[dy][dx] (src/render.c:49)
-        auto offs = [](int i, int j, int& ox, int& oy) {
-            ox = SEM == kSemLqr ? i : j;
-            oy = SEM == kSemLqr ? j : i;
         };
 
         if (cnt <= kFixDirect) {
-            // sparse tile: windows straight from global memory
+            // sparse strip: windows straight from global memory
             if constexpr (N <= 8) {
-                if ((unsigned)tx < cnt) {
-                    const unsigned loc = list[tx];
-                    const int ly = (int)(loc / TW), lx = (int)(loc % TW);
+                if ((unsigned)lane < cnt) {
+                    const unsigned loc = list[lane];
+                    const int ly = (int)(loc >> 6), lx = (int)(loc & 63);
                     double d[N * N];
 #pragma unroll
                     for (int i = 0; i < N; i++)
@@ -672,7 +762,7 @@ __global__ __launch_bounds__(kFixThreads, DCTE_FIX_WAVES) void dcte_fix_tiles(co
                         for (int j = 0; j < N; j++) {
                             int ox, oy;
                             offs(i, j, ox, oy);
-                            d[i * N + j] = luma(pixel(clampi(x0 + lx + ox - HL, 0, p.w - 1),
+                            d[i * N + j] = luma(pixel(clampi(sx0 + lx + ox - HL, 0, p.w - 1),
                                                       clampi(ys + ly + oy - HL, 0, p.h - 1)));
                         }
                     double m;
@@ -681,21 +771,21 @@ __global__ __launch_bounds__(kFixThreads, DCTE_FIX_WAVES) void dcte_fix_tiles(co
                     store(lx, ly, m, edge);
                 }
             } else {
-                const int l = tx & 15, slot = tx >> 4;
-                double* d = win[slot];
-                for (unsigned r0 = 0; r0 < cnt; r0 += NW) {           // uniform
-                    const unsigned q = r0 + slot;
+                const int l = lane & 15, grp = lane >> 4;
+                double* d = win[grp];
+                for (unsigned r0 = 0; r0 < cnt; r0 += 4) {            // uniform
+                    const unsigned q = r0 + grp;
                     const bool valid = q < cnt;
                     int lx = 0, ly = 0;
                     if (valid) {
                         const unsigned loc = list[q];
-                        ly = (int)(loc / TW);
-                        lx = (int)(loc % TW);
+                        ly = (int)(loc >> 6);
+                        lx = (int)(loc & 63);
 #pragma unroll
                         for (int t = 0; t < 16; t++) {
                             int ox, oy;
                             offs(t, l, ox, oy);
-                            d[t * 16 + l] = luma(pixel(clampi(x0 + lx + ox - HL, 0, p.w - 1),
+                            d[t * 16 + l] = luma(pixel(clampi(sx0 + lx + ox - HL, 0, p.w - 1),
                                                        clampi(ys + ly + oy - HL, 0, p.h - 1)));
                         }
                     }
@@ -710,134 +800,65 @@ __global__ __launch_bounds__(kFixThreads, DCTE_FIX_WAVES) void dcte_fix_tiles(co
             continue;
         }
 
-        // dense tile: sub-band ranges of the list.  Output row ly was emitted
-        // in map group (ly + N - 1) / G; sub-band = group / GPS.
-        if (tx < NSB) sb_n[tx] = 0;
-        __syncthreads();
-        for (unsigned q = tx; q < cnt; q += kFixThreads) {
-            const int ly = (int)(list[q] / TW);
-            atomicAdd(&sb_n[((ly + N - 1) / G) / FT::GPS], 1u);
-        }
-        __syncthreads();
-        if (tx == 0) {
-            unsigned acc = 0;
-            for (int b = 0; b < NSB; b++) {
-                sb_off[b] = acc;
-                acc += sb_n[b];
-            }
-            sb_off[NSB] = acc;
-        }
-        __syncthreads();
-        // whole rows of the span are contiguous unless the tile touches the
-        // left / right frame border (3 spare bytes: the last dword stays in the row)
-        const bool interior = x0 - HL >= 0 && (x0 - HL + LW) * BPP + 3 <= p.w * BPP;
-        // sub-band b: output rows [max(A, 0), min(A + SBH, ye - ys)), A = b SBH - (N - 1);
-        // input rows from r0 = max(A, 0) - HL (tile-relative)
-        auto band_rows = [&](int b, int& r0, int& nrows) {
-            const int A = b * SBH - (N - 1);
-            r0 = max(A, 0) - HL;
-            nrows = min(A + SBH, ye - ys) - max(A, 0) + N - 1;
+        // dense strip, band by band.  Output row ly was emitted in map group
+        // (ly + N - 1) / G; band = group / GPS, output rows [A, A + SBH) with
+        // A = band SBH - (N - 1); its input rows start at r0 = max(A, 0) - HL.
+        const bool interior = sx0 - HL >= 0 && (sx0 - HL + LW) * BPP + 3 <= p.w * BPP;
+        int staged = -1, r0 = 0;
+        auto band_of = [](int ly) { return ((ly + N - 1) / G) / FS::GPS; };
+        auto stage = [&](int b) {
+            r0 = fix_stage_band<N, BPP, SEM>(p, rsrc, base_off, lut, lum, raw, mis, b, sx0, ys, ye,
+                                             interior, lane);
+            staged = b;
         };
-        // raw dwords of a sub-band's rows (interior tiles), all loads in flight
-        // at once; they land in registers while the previous sub-band computes
-        constexpr int SPAN = LW * BPP;
-        constexpr int U = (LR * PDW + kFixThreads - 1) / kFixThreads;
-        uint32_t v[U];
-        auto issue = [&](int b) {
-            int r0, nrows;
-            band_rows(b, r0, nrows);
+        // element (i, j) of pixel (lx, ly): lum row ly + oy - HL - r0, column lx + ox
+        if constexpr (N <= 8) {
+            for (unsigned c0 = 0; c0 < cnt; c0 += 64) {
+                const unsigned q = c0 + lane;
+                const bool valid = q < cnt;
+                const unsigned loc = valid ? list[q] : 0u;
+                const int ly = (int)(loc >> 6), lx = (int)(loc & 63);
+                const int key = valid ? band_of(ly) : kBig;
+                bool pending = valid;
+                for (;;) {
+                    const int kmin = wave_min(pending ? key : kBig);      // uniform
+                    if (kmin == kBig) break;
+                    if (kmin != staged) stage(kmin);
+                    if (pending && key == kmin) {
+                        const double* base = &lum[(ly - HL - r0) * LW + lx];
+                        double d[N * N];
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int e = tx + u * kFixThreads;
-                const int r = e / PDW, dw = e - r * PDW;
-                v[u] = 0;
-                if (r < nrows) {
-                    const int gy = clampi(ys + r0 + r, 0, p.h - 1);
-                    const uint32_t a = base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
-                                       (uint32_t)((x0 - HL) * BPP);
-                    if (dw * 4 < (int)(a & 3u) + SPAN)
-                        v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)((a & ~3u) + 4u * dw), 0, 0);
-                }
-            }
-        };
-        auto next_band = [&](int b) {
-            for (b = b + 1; b < NSB; b++)
-                if (sb_off[b] != sb_off[b + 1]) return b;
-            return NSB;
-        };
-        int b = next_band(-1);
-        if (interior && b < NSB) issue(b);
-        for (; b < NSB; ) {
-            const unsigned q0 = sb_off[b], q1 = sb_off[b + 1];
-            int r0, nrows;
-            band_rows(b, r0, nrows);
-            __syncthreads();                           // the previous sub-band's reads are done
-            if (interior) {
+                        for (int i = 0; i < N; i++)
 #pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const int e = tx + u * kFixThreads;
-                    const int r = e / PDW;
-                    if (r < nrows) {
-                        raw[e] = v[u];
-                        if (e - r * PDW == 0) {
-                            const int gy = clampi(ys + r0 + r, 0, p.h - 1);
-                            mis[r] = (unsigned char)((base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
-                                                      (uint32_t)((x0 - HL) * BPP)) & 3u);
-                        }
+                            for (int j = 0; j < N; j++) {
+                                int ox, oy;
+                                offs(i, j, ox, oy);
+                                d[i * N + j] = base[oy * LW + ox];
+                            }
+                        double m;
+                        bool edge;
+                        refine_regs<N>(d, tp.ct, m, edge);
+                        store(lx, ly, m, edge);
+                        pending = false;
                     }
                 }
-            } else {
-                for (int e = tx; e < nrows * LW; e += kFixThreads) {
-                    const int r = e / LW, c = e - r * LW;
-                    const uint8_t* src = pixel(clampi(x0 - HL + c, 0, p.w - 1), clampi(ys + r0 + r, 0, p.h - 1));
-                    uint8_t* dst = reinterpret_cast<uint8_t*>(&raw[r * PDW]) + c * BPP;
-#pragma unroll
-                    for (int ch = 0; ch < BPP; ch++) dst[ch] = src[ch];
-                    if (c == 0) mis[r] = 0;
-                }
             }
-            __syncthreads();
-            for (int e = tx; e < nrows * LW; e += kFixThreads) {
-                const int r = e / LW, c = e - r * LW;
-                lum[r * LW + c] = luma(reinterpret_cast<const uint8_t*>(&raw[r * PDW]) + mis[r] + c * BPP);
-            }
-            const int bn = next_band(b);
-            if (interior && bn < NSB) issue(bn);       // lands during this sub-band's compute
-            __syncthreads();
-            // element (i, j) of pixel (lx, ly): lum row ly + oy - HL - r0, column lx + ox
-            if constexpr (N <= 8) {
-                // entries dealt round-robin over the four waves (a sub-band
-                // often holds fewer than 256: all SIMDs get a share)
-                const int slot = (tx & 63) * 4 + (tx >> 6);
-                for (unsigned q = q0 + slot; q < q1; q += kFixThreads) {
-                    const unsigned loc = list[q];
-                    const int ly = (int)(loc / TW), lx = (int)(loc % TW);
-                    const double* base = &lum[(ly - HL - r0) * LW + lx];
-                    double d[N * N];
-#pragma unroll
-                    for (int i = 0; i < N; i++)
-#pragma unroll
-                        for (int j = 0; j < N; j++) {
-                            int ox, oy;
-                            offs(i, j, ox, oy);
-                            d[i * N + j] = base[oy * LW + ox];
-                        }
-                    double m;
-                    bool edge;
-                    refine_regs<N>(d, tp.ct, m, edge);
-                    store(lx, ly, m, edge);
-                }
-            } else {
-                const int l = tx & 15, slot = (tx >> 4 & 3) * 4 + (tx >> 6);   // groups round-robin over waves
-                double* d = win[tx >> 4];
-                for (unsigned rq = q0; rq < q1; rq += NW) {            // uniform
-                    const unsigned q = rq + slot;
-                    const bool valid = q < q1;
-                    int lx = 0, ly = 0;
-                    if (valid) {
-                        const unsigned loc = list[q];
-                        ly = (int)(loc / TW);
-                        lx = (int)(loc % TW);
+        } else {
+            const int l = lane & 15, grp = lane >> 4;
+            double* d = win[grp];
+            for (unsigned c0 = 0; c0 < cnt; c0 += 4) {
+                const unsigned q = c0 + grp;
+                const bool valid = q < cnt;
+                const unsigned loc = valid ? list[q] : 0u;
+                const int ly = (int)(loc >> 6), lx = (int)(loc & 63);
+                const int key = valid ? band_of(ly) : kBig;
+                bool pending = valid;
+                for (;;) {
+                    const int kmin = wave_min(pending ? key : kBig);      // uniform
+                    if (kmin == kBig) break;
+                    if (kmin != staged) stage(kmin);
+                    const bool mine = pending && key == kmin;
+                    if (mine) {
                         const double* base = &lum[(ly - HL - r0) * LW + lx];
 #pragma unroll
                         for (int t = 0; t < 16; t++) {
@@ -850,13 +871,12 @@ __global__ __launch_bounds__(kFixThreads, DCTE_FIX_WAVES) void dcte_fix_tiles(co
                     double best;
                     bool edge;
                     refine16_group(d, l, best, edge);
-                    if (valid && l == 0) store(lx, ly, best, edge);
+                    if (mine && l == 0) store(lx, ly, best, edge);
                     wave_sync_lds();
+                    if (mine) pending = false;
                 }
             }
-            b = bn;
         }
-        __syncthreads();                               // sb_n / raw / lum reuse by the next tile
     }
 }
 
@@ -869,6 +889,7 @@ int map_tile_w(int n)
 int map_default_tile_h(int n) { return n == 16 ? DCTE_TILE_H16 : DCTE_TILE_H; }
 int map_tiles_x(int n, int w) { return (w + map_tile_w(n) - 1) / map_tile_w(n); }
 int map_tiles_y(int n, int rows) { return (rows + map_default_tile_h(n) - 1) / map_default_tile_h(n); }
+int map_strips_per_tile(int n) { return n == 16 ? 1 : map_tile_w(n) / 64; }
 
 template <int N, int BPP, int SEM>
 static hipError_t launch_map_t(const MapParams& p, hipStream_t s)
@@ -922,11 +943,11 @@ static void launch_fix_n(const FixParams& p, hipStream_t s)
 template <int N, int BPP, int SEM>
 static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
 {
-    if (p.m.tile_h != FixTile<N, SEM>::TH || p.tiles_x != (p.m.w + Geo<N, SEM>::TW - 1) / Geo<N, SEM>::TW)
+    if (p.m.tile_h != FixStrip<N, SEM>::TH || p.tiles_x != (p.m.w + Geo<N, SEM>::TW - 1) / Geo<N, SEM>::TW)
         return hipErrorInvalidValue;
-    const int ntiles = p.tiles_x * ((p.m.y1 - p.m.y0 + p.m.tile_h - 1) / p.m.tile_h);
-    const int blocks = ntiles < 1024 ? ntiles : 1024;  // 1-2 resident per CU (LDS), 2 rounds
-    hipLaunchKernelGGL((dcte_fix_tiles<N, BPP, SEM>), dim3(blocks), dim3(kFixThreads), 0, s, p);
+    const int nstrips = p.tiles_x * FixStrip<N, SEM>::SPT * ((p.m.y1 - p.m.y0 + p.m.tile_h - 1) / p.m.tile_h);
+    const int blocks = nstrips < 2048 ? nstrips : 2048;   // one wave each; ~6-8 per CU
+    hipLaunchKernelGGL((dcte_fix_strips<N, BPP, SEM>), dim3(blocks), dim3(64), 0, s, p);
     return hipGetLastError();
 }
 
