@@ -600,8 +600,8 @@ struct FixStrip {
     static constexpr int SPT = Lanes<N>::S == 1 ? Geo<N, SEM>::TW / 64 : 1;   // strips per tile
     static constexpr int LW = 64 + N - 1;             // luma columns of a strip
     static constexpr int G = Geo<N, SEM>::G;          // map kernel rows per group
-    static constexpr int GPS = N == 16 ? 1 : 3;       // groups per band
-    static constexpr int SBH = GPS * G;               // output rows per band (24; N = 16: 16)
+    static constexpr int GPS = 1;                     // groups per band
+    static constexpr int SBH = GPS * G;               // output rows per band (8; N = 16: 16)
     static constexpr int LR = SBH + N - 1;            // input rows staged per band
 };
 
@@ -612,80 +612,52 @@ __device__ __forceinline__ int wave_min(int v)
     return v;
 }
 
-// dcte_fix_strips: stage band b of a strip -- its input rows + window halo
-// as raw bytes (coalesced dwords; clamped per pixel at the left / right
-// frame border), then as the reference's fp64 luma -- in this wave's LDS.
-// Returns the band's first input row (tile-relative).  Not inlined: the
-// band is staged a few times per strip, and inlined into the refinement loop
-// its loads-in-flight share registers with the 64-element window.
-template <int N, int BPP, int SEM>
-__device__ __noinline__ int fix_stage_band(const MapParams& p, __amdgpu_buffer_rsrc_t rsrc,
-                                           uint32_t base_off, const double* lut, double* lum,
-                                           uint32_t* raw, unsigned char* mis, int b, int sx0, int ys,
-                                           int ye, bool interior, int lane)
+// One pixel's refinement by a group of N lanes (N = 8, 16) from the band's
+// fp64 luma in LDS: lane l runs the reference's first pass on window line l
+// (ddct8x8s / ddct16x16s transform along the first index for each second
+// index), the lines meet in the group's window buffer w, lane l runs the
+// second pass on coefficient row l and scans it (last maximum,
+// src/dct.c:103), and the group reduces (larger index wins ties).  `at` =
+// the lum index of window element (0, 0).  Every lane of the wave calls it.
+template <int N, int SEM>
+__device__ __forceinline__ void refine_group(const double* lum, int LW, int at, double* w, int l,
+                                             double& best, bool& edge)
 {
-    using FS = FixStrip<N, SEM>;
-    constexpr int LW = FS::LW, SBH = FS::SBH, LR = FS::LR;
-    constexpr int HL = Geo<N, SEM>::HL;
-    constexpr int PDW = (((LW * BPP + 3) & ~3) + 4) / 4;
-    const int A = b * SBH - (N - 1);
-    const int r0 = max(A, 0) - HL;
-    const int nrows = min(A + SBH, ye - ys) - max(A, 0) + N - 1;
-    wave_sync_lds();                               // the previous band's reads are done
-    if (interior) {
-        // every load of the band in flight at once, then the LDS stores
-        constexpr int SPAN = LW * BPP;
-        constexpr int U = (LR * PDW + 63) / 64;
-        uint32_t v[U];
+    double v[N];
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int e = lane + 64 * u;
-            const int r = e / PDW, dw = e - r * PDW;
-            v[u] = 0;
-            if (r < nrows) {
-                const int gy = clampi(ys + r0 + r, 0, p.h - 1);
-                const uint32_t a = base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
-                                   (uint32_t)((sx0 - HL) * BPP);
-                if (dw == 0) mis[r] = (unsigned char)(a & 3u);
-                if (dw * 4 < (int)(a & 3u) + SPAN)
-                    v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)((a & ~3u) + 4u * dw), 0, 0);
-            }
-        }
+    for (int i = 0; i < N; i++)   // d[i][l]: liblqr data[dx][dy] (row l, column i); preview data[dy][dx]
+        v[i] = SEM == kSemLqr ? lum[at + l * LW + i] : lum[at + i * LW + l];
+    if constexpr (N == 8) r64::step8(v, 1); else r64::step16(v, 1);
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int e = lane + 64 * u;
-            if (e < nrows * PDW) raw[e] = v[u];
-        }
-    } else {
-        for (int e = lane; e < nrows * LW; e += 64) {
-            const int r = e / LW, c = e - r * LW;
-            const uint8_t* src = p.px + (long long)(clampi(ys + r0 + r, 0, p.h - 1) - p.in_row0) * p.rowstride +
-                                 (long long)clampi(sx0 - HL + c, 0, p.w - 1) * BPP;
-            uint8_t* dst = reinterpret_cast<uint8_t*>(&raw[r * PDW]) + c * BPP;
-#pragma unroll
-            for (int ch = 0; ch < BPP; ch++) dst[ch] = src[ch];
-            if (c == 0) mis[r] = 0;
-        }
-    }
+    for (int i = 0; i < N; i++) w[i * N + l] = v[i];
     wave_sync_lds();
-    for (int e = lane; e < nrows * LW; e += 64) {
-        const int r = e / LW, c = e - r * LW;
-        const uint8_t* q = reinterpret_cast<const uint8_t*>(&raw[r * PDW]) + mis[r] + c * BPP;
-        double L;
-        if constexpr (SEM == kSemLqr) {
-            if constexpr (BPP == 1) L = lut[q[0]];
-            else L = 0.2126 * lut[q[0]] + 0.7152 * lut[q[1]] + 0.0722 * lut[q[2]];
-        } else {
-            L = (double)preview_luma(q[0], BPP > 1 ? q[1] : 0u, BPP > 1 ? q[2] : 0u, BPP);
-        }
-        lum[r * LW + c] = L;
+#pragma unroll
+    for (int k = 0; k < N; k++) v[k] = w[l * N + k];
+    wave_sync_lds();                                   // w may be refilled after this
+    if constexpr (N == 8) r64::step8(v, 1); else r64::step16(v, 1);
+    best = -1.0;
+    int bi = -1;
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        const int e = l * N + k;
+        const double a = fabs(v[k]);
+        const bool take = e != 0 && a >= best;
+        best = take ? a : best;
+        bi = take ? e : bi;
     }
-    wave_sync_lds();
-    return r0;
+#pragma unroll
+    for (int o = N / 2; o > 0; o >>= 1) {
+        const double ob = __shfl_xor(best, o, N);
+        const int oi = __shfl_xor(bi, o, N);
+        const bool take = ob > best || (ob == best && oi > bi);
+        best = take ? ob : best;
+        bi = take ? oi : bi;
+    }
+    edge = bi == 1 || bi == N;
 }
 
 template <int N, int BPP, int SEM>
-__global__ __launch_bounds__(64, 2) void dcte_fix_strips(const TileFixParams tp)
+__global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
 {
     using FS = FixStrip<N, SEM>;
     constexpr int TH = FS::TH, SPT = FS::SPT, LW = FS::LW, G = FS::G, SBH = FS::SBH, LR = FS::LR;
@@ -693,12 +665,14 @@ __global__ __launch_bounds__(64, 2) void dcte_fix_strips(const TileFixParams tp)
     constexpr int HL = Geo<N, SEM>::HL;
     constexpr int PB = ((LW * BPP + 3) & ~3) + 4;      // raw row pitch: the span + misalignment
     constexpr int PDW = PB / 4;
-    constexpr int kBig = 1 << 30;
+    constexpr bool kGroup = N >= 8;                    // N lanes per pixel (else one lane)
+    constexpr int PPW = kGroup ? 64 / N : 64;          // pixels per wave pass
     __shared__ double lut[256];
-    __shared__ double lum[LR * LW];                    // fp64 luma of one band (+ halo)
+    __shared__ double lum[LR * LW];                    // fp64 luma of one band (+ halo), needed columns
     __shared__ __attribute__((aligned(16))) uint32_t raw[LR * PDW];
     __shared__ unsigned char mis[LR];                  // byte offset of each raw row's first pixel
-    __shared__ double win[N == 16 ? 4 : 1][N == 16 ? 256 : 1];
+    __shared__ unsigned char colidx[LW];               // the needed luma columns, ascending
+    __shared__ double win[kGroup ? PPW : 1][kGroup ? N * N : 1];
     const MapParams& p = tp.m;
     const unsigned ndirty = *p.dirty_count;
     if (blockIdx.x >= ndirty) return;                  // uniform
@@ -734,6 +708,7 @@ __global__ __launch_bounds__(64, 2) void dcte_fix_strips(const TileFixParams tp)
         ox = SEM == kSemLqr ? i : j;
         oy = SEM == kSemLqr ? j : i;
     };
+    auto band_of = [](unsigned loc) { return (((int)(loc >> 6) + N - 1) / G) / FS::GPS; };
 
     for (unsigned k = blockIdx.x; k < ndirty; k += gridDim.x) {
         const unsigned strip = p.dirty_list[k];
@@ -751,7 +726,7 @@ __global__ __launch_bounds__(64, 2) void dcte_fix_strips(const TileFixParams tp)
 
         if (cnt <= kFixDirect) {
             // sparse strip: windows straight from global memory
-            if constexpr (N <= 8) {
+            if constexpr (!kGroup) {
                 if ((unsigned)lane < cnt) {
                     const unsigned loc = list[lane];
                     const int ly = (int)(loc >> 6), lx = (int)(loc & 63);
@@ -771,10 +746,11 @@ __global__ __launch_bounds__(64, 2) void dcte_fix_strips(const TileFixParams tp)
                     store(lx, ly, m, edge);
                 }
             } else {
-                const int l = lane & 15, grp = lane >> 4;
+                // group g: pixel q0 + g; lane l gathers window line l
+                const int l = lane & (N - 1), grp = lane / N;
                 double* d = win[grp];
-                for (unsigned r0 = 0; r0 < cnt; r0 += 4) {            // uniform
-                    const unsigned q = r0 + grp;
+                for (unsigned q0 = 0; q0 < cnt; q0 += PPW) {          // uniform
+                    const unsigned q = q0 + grp;
                     const bool valid = q < cnt;
                     int lx = 0, ly = 0;
                     if (valid) {
@@ -782,100 +758,169 @@ __global__ __launch_bounds__(64, 2) void dcte_fix_strips(const TileFixParams tp)
                         ly = (int)(loc >> 6);
                         lx = (int)(loc & 63);
 #pragma unroll
-                        for (int t = 0; t < 16; t++) {
+                        for (int t = 0; t < N; t++) {
                             int ox, oy;
                             offs(t, l, ox, oy);
-                            d[t * 16 + l] = luma(pixel(clampi(sx0 + lx + ox - HL, 0, p.w - 1),
-                                                       clampi(ys + ly + oy - HL, 0, p.h - 1)));
+                            d[t * N + l] = luma(pixel(clampi(sx0 + lx + ox - HL, 0, p.w - 1),
+                                                      clampi(ys + ly + oy - HL, 0, p.h - 1)));
                         }
                     }
                     wave_sync_lds();
-                    double best;
-                    bool edge;
-                    refine16_group(d, l, best, edge);
-                    if (valid && l == 0) store(lx, ly, best, edge);
+                    // the group transforms its window in place (d[i][j] = d[i * N + j])
+                    if constexpr (N == 8) r64::step8(d + l, 8); else r64::step16(d + l, 16);
+                    wave_sync_lds();
+                    if constexpr (N == 8) r64::step8(d + N * l, 1); else r64::step16(d + N * l, 1);
+                    wave_sync_lds();
+                    double best = -1.0;
+                    int bi = -1;
+#pragma unroll
+                    for (int c = 0; c < N; c++) {
+                        const int e = l * N + c;
+                        const double a = fabs(d[e]);
+                        const bool take = e != 0 && a >= best;
+                        best = take ? a : best;
+                        bi = take ? e : bi;
+                    }
+#pragma unroll
+                    for (int o = N / 2; o > 0; o >>= 1) {
+                        const double ob = __shfl_xor(best, o, N);
+                        const int oi = __shfl_xor(bi, o, N);
+                        const bool take = ob > best || (ob == best && oi > bi);
+                        best = take ? ob : best;
+                        bi = take ? oi : bi;
+                    }
+                    if (valid && l == 0) store(lx, ly, best, bi == 1 || bi == N);
                     wave_sync_lds();
                 }
             }
             continue;
         }
 
-        // dense strip, band by band.  Output row ly was emitted in map group
-        // (ly + N - 1) / G; band = group / GPS, output rows [A, A + SBH) with
-        // A = band SBH - (N - 1); its input rows start at r0 = max(A, 0) - HL.
+        // dense strip, band by band.  The entries are sorted by band (the map
+        // kernel emits them group by group; band = group / GPS), so a band's
+        // entries are a contiguous run [pos, end) of the list.
         const bool interior = sx0 - HL >= 0 && (sx0 - HL + LW) * BPP + 3 <= p.w * BPP;
-        int staged = -1, r0 = 0;
-        auto band_of = [](int ly) { return ((ly + N - 1) / G) / FS::GPS; };
-        auto stage = [&](int b) {
-            r0 = fix_stage_band<N, BPP, SEM>(p, rsrc, base_off, lut, lum, raw, mis, b, sx0, ys, ye,
-                                             interior, lane);
-            staged = b;
-        };
-        // element (i, j) of pixel (lx, ly): lum row ly + oy - HL - r0, column lx + ox
-        if constexpr (N <= 8) {
-            for (unsigned c0 = 0; c0 < cnt; c0 += 64) {
-                const unsigned q = c0 + lane;
-                const bool valid = q < cnt;
-                const unsigned loc = valid ? list[q] : 0u;
-                const int ly = (int)(loc >> 6), lx = (int)(loc & 63);
-                const int key = valid ? band_of(ly) : kBig;
-                bool pending = valid;
-                for (;;) {
-                    const int kmin = wave_min(pending ? key : kBig);      // uniform
-                    if (kmin == kBig) break;
-                    if (kmin != staged) stage(kmin);
-                    if (pending && key == kmin) {
-                        const double* base = &lum[(ly - HL - r0) * LW + lx];
-                        double d[N * N];
+        for (unsigned pos = 0; pos < cnt;) {                           // uniform
+            const int b = band_of(list[pos]);
+            // the run's end and the luma columns its windows need (bits of a 96-bit mask)
+            unsigned end = pos;
+            uint32_t m0 = 0, m1 = 0, m2 = 0;
+            for (;;) {
+                const unsigned q = end + lane;
+                const unsigned loc = q < cnt ? list[q] : 0u;
+                const bool in = q < cnt && band_of(loc) == b;
+                if (in) {
+                    const int lx = (int)(loc & 63);
 #pragma unroll
-                        for (int i = 0; i < N; i++)
-#pragma unroll
-                            for (int j = 0; j < N; j++) {
-                                int ox, oy;
-                                offs(i, j, ox, oy);
-                                d[i * N + j] = base[oy * LW + ox];
-                            }
-                        double m;
-                        bool edge;
-                        refine_regs<N>(d, tp.ct, m, edge);
-                        store(lx, ly, m, edge);
-                        pending = false;
+                    for (int o = 0; o < N; o++) {
+                        const int c = lx + o;
+                        if (c < 32) m0 |= 1u << c;
+                        else if (c < 64) m1 |= 1u << (c - 32);
+                        else m2 |= 1u << (c - 64);
                     }
                 }
+                const int nin = __popcll(__ballot(in));     // a prefix of the lanes
+                end += nin;
+                if (nin < 64) break;
             }
-        } else {
-            const int l = lane & 15, grp = lane >> 4;
-            double* d = win[grp];
-            for (unsigned c0 = 0; c0 < cnt; c0 += 4) {
-                const unsigned q = c0 + grp;
-                const bool valid = q < cnt;
-                const unsigned loc = valid ? list[q] : 0u;
-                const int ly = (int)(loc >> 6), lx = (int)(loc & 63);
-                const int key = valid ? band_of(ly) : kBig;
-                bool pending = valid;
-                for (;;) {
-                    const int kmin = wave_min(pending ? key : kBig);      // uniform
-                    if (kmin == kBig) break;
-                    if (kmin != staged) stage(kmin);
-                    const bool mine = pending && key == kmin;
-                    if (mine) {
-                        const double* base = &lum[(ly - HL - r0) * LW + lx];
 #pragma unroll
-                        for (int t = 0; t < 16; t++) {
-                            int ox, oy;
-                            offs(t, l, ox, oy);
-                            d[t * 16 + l] = base[oy * LW + ox];
-                        }
+            for (int o = 32; o > 0; o >>= 1) {
+                m0 |= __shfl_xor(m0, o);
+                m1 |= __shfl_xor(m1, o);
+                m2 |= __shfl_xor(m2, o);
+            }
+            // band b: output rows [max(A, 0), min(A + SBH, ye - ys)), A = b SBH - (N - 1);
+            // input rows from r0 = max(A, 0) - HL (tile-relative)
+            const int A = b * SBH - (N - 1);
+            const int r0 = max(A, 0) - HL;
+            const int nrows = min(A + SBH, ye - ys) - max(A, 0) + N - 1;
+            // raw bytes of the band's rows
+            if (interior) {
+                constexpr int SPAN = LW * BPP;
+                constexpr int U = (LR * PDW + 63) / 64;
+                uint32_t v[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int e = lane + 64 * u;
+                    const int r = e / PDW, dw = e - r * PDW;
+                    v[u] = 0;
+                    if (r < nrows) {
+                        const int gy = clampi(ys + r0 + r, 0, p.h - 1);
+                        const uint32_t a = base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
+                                           (uint32_t)((sx0 - HL) * BPP);
+                        if (dw == 0) mis[r] = (unsigned char)(a & 3u);
+                        if (dw * 4 < (int)(a & 3u) + SPAN)
+                            v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)((a & ~3u) + 4u * dw), 0, 0);
                     }
-                    wave_sync_lds();
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int e = lane + 64 * u;
+                    if (e < nrows * PDW) raw[e] = v[u];
+                }
+            } else {
+                for (int e = lane; e < nrows * LW; e += 64) {
+                    const int r = e / LW, c = e - r * LW;
+                    const uint8_t* src = pixel(clampi(sx0 - HL + c, 0, p.w - 1), clampi(ys + r0 + r, 0, p.h - 1));
+                    uint8_t* dst = reinterpret_cast<uint8_t*>(&raw[r * PDW]) + c * BPP;
+#pragma unroll
+                    for (int ch = 0; ch < BPP; ch++) dst[ch] = src[ch];
+                    if (c == 0) mis[r] = 0;
+                }
+            }
+            // the needed columns, compacted
+            const int n0 = __popc(m0), n1 = __popc(m1);
+            const int ncols = n0 + n1 + __popc(m2);
+            for (int c = lane; c < LW; c += 64) {
+                const uint32_t word = c < 32 ? m0 : (c < 64 ? m1 : m2);
+                const int bit = c & 31;
+                if ((word >> bit) & 1u) {
+                    const int before = (c < 32 ? 0 : (c < 64 ? n0 : n0 + n1)) +
+                                       __popc(word & ((1u << bit) - 1u));
+                    colidx[before] = (unsigned char)c;
+                }
+            }
+            wave_sync_lds();
+            for (int e = lane; e < nrows * ncols; e += 64) {
+                const int r = e / ncols, c = colidx[e - r * ncols];
+                lum[r * LW + c] = luma(reinterpret_cast<const uint8_t*>(&raw[r * PDW]) + mis[r] + c * BPP);
+            }
+            wave_sync_lds();
+            // element (i, j) of pixel (lx, ly): lum row ly + oy - HL - r0, column lx + ox
+            if constexpr (!kGroup) {
+                for (unsigned q = pos + lane; q < end; q += 64) {
+                    const unsigned loc = list[q];
+                    const int ly = (int)(loc >> 6), lx = (int)(loc & 63);
+                    const double* base = &lum[(ly - HL - r0) * LW + lx];
+                    double d[N * N];
+#pragma unroll
+                    for (int i = 0; i < N; i++)
+#pragma unroll
+                        for (int j = 0; j < N; j++) {
+                            int ox, oy;
+                            offs(i, j, ox, oy);
+                            d[i * N + j] = base[oy * LW + ox];
+                        }
+                    double m;
+                    bool edge;
+                    refine_regs<N>(d, tp.ct, m, edge);
+                    store(lx, ly, m, edge);
+                }
+            } else {
+                const int l = lane & (N - 1), grp = lane / N;
+                for (unsigned q0 = pos; q0 < end; q0 += PPW) {        // uniform
+                    const unsigned q = q0 + grp;
+                    const bool valid = q < end;
+                    const unsigned loc = valid ? list[q] : list[pos];
+                    const int ly = (int)(loc >> 6), lx = (int)(loc & 63);
                     double best;
                     bool edge;
-                    refine16_group(d, l, best, edge);
-                    if (mine && l == 0) store(lx, ly, best, edge);
-                    wave_sync_lds();
-                    if (mine) pending = false;
+                    refine_group<N, SEM>(lum, LW, (ly - HL - r0) * LW + lx, win[grp], l, best, edge);
+                    if (valid && l == 0) store(lx, ly, best, edge);
                 }
             }
+            wave_sync_lds();                           // lum / raw / colidx free for the next band
+            pos = end;
         }
     }
 }
