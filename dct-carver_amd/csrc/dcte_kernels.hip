@@ -600,8 +600,11 @@ struct FixStrip {
     static constexpr int SPT = Lanes<N>::S == 1 ? Geo<N, SEM>::TW / 64 : 1;   // strips per tile
     static constexpr int LW = 64 + N - 1;             // luma columns of a strip
     static constexpr int G = Geo<N, SEM>::G;          // map kernel rows per group
-    static constexpr int GPS = 1;                     // groups per band
-    static constexpr int SBH = GPS * G;               // output rows per band (8; N = 16: 16)
+#ifndef DCTE_FIX_GPS
+#define DCTE_FIX_GPS 2
+#endif
+    static constexpr int GPS = N == 16 ? 1 : DCTE_FIX_GPS;   // map row groups per band
+    static constexpr int SBH = GPS * G;               // output rows per band (16)
     static constexpr int LR = SBH + N - 1;            // input rows staged per band
 };
 
