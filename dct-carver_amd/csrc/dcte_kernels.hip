@@ -621,7 +621,9 @@ __device__ __forceinline__ int wave_min(int v)
 // index), the lines meet in the group's window buffer w, lane l runs the
 // second pass on coefficient row l and scans it (last maximum,
 // src/dct.c:103), and the group reduces (larger index wins ties).  `at` =
-// the lum index of window element (0, 0).  Every lane of the wave calls it.
+// the lum index of window element (0, 0); w holds N rows of N + 1 doubles
+// (the pad keeps both passes' accesses on distinct LDS banks).  Every lane
+// of the wave calls it.
 template <int N, int SEM>
 __device__ __forceinline__ void refine_group(const double* lum, int LW, int at, double* w, int l,
                                              double& best, bool& edge)
@@ -632,10 +634,10 @@ __device__ __forceinline__ void refine_group(const double* lum, int LW, int at, 
         v[i] = SEM == kSemLqr ? lum[at + l * LW + i] : lum[at + i * LW + l];
     if constexpr (N == 8) r64::step8(v, 1); else r64::step16(v, 1);
 #pragma unroll
-    for (int i = 0; i < N; i++) w[i * N + l] = v[i];
+    for (int i = 0; i < N; i++) w[i * (N + 1) + l] = v[i];   // rows padded: no bank conflicts
     wave_sync_lds();
 #pragma unroll
-    for (int k = 0; k < N; k++) v[k] = w[l * N + k];
+    for (int k = 0; k < N; k++) v[k] = w[l * (N + 1) + k];
     wave_sync_lds();                                   // w may be refilled after this
     if constexpr (N == 8) r64::step8(v, 1); else r64::step16(v, 1);
     best = -1.0;
@@ -675,7 +677,10 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
     __shared__ __attribute__((aligned(16))) uint32_t raw[LR * PDW];
     __shared__ unsigned char mis[LR];                  // byte offset of each raw row's first pixel
     __shared__ unsigned char colidx[LW];               // the needed luma columns, ascending
-    __shared__ double win[kGroup ? PPW : 1][kGroup ? N * N : 1];
+    // per group: N rows of N + 1 doubles, plus a pad that starts consecutive
+    // groups 16 banks apart
+    constexpr int WS = kGroup ? (N * (N + 1) + 7) / 8 * 8 + 8 : 1;
+    __shared__ double win[kGroup ? PPW : 1][WS];
     const MapParams& p = tp.m;
     const unsigned ndirty = *p.dirty_count;
     if (blockIdx.x >= ndirty) return;                  // uniform
@@ -764,22 +769,22 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
                         for (int t = 0; t < N; t++) {
                             int ox, oy;
                             offs(t, l, ox, oy);
-                            d[t * N + l] = luma(pixel(clampi(sx0 + lx + ox - HL, 0, p.w - 1),
-                                                      clampi(ys + ly + oy - HL, 0, p.h - 1)));
+                            d[t * (N + 1) + l] = luma(pixel(clampi(sx0 + lx + ox - HL, 0, p.w - 1),
+                                                            clampi(ys + ly + oy - HL, 0, p.h - 1)));
                         }
                     }
                     wave_sync_lds();
-                    // the group transforms its window in place (d[i][j] = d[i * N + j])
-                    if constexpr (N == 8) r64::step8(d + l, 8); else r64::step16(d + l, 16);
+                    // the group transforms its window in place (d[i][j] = d[i * (N + 1) + j])
+                    if constexpr (N == 8) r64::step8(d + l, N + 1); else r64::step16(d + l, N + 1);
                     wave_sync_lds();
-                    if constexpr (N == 8) r64::step8(d + N * l, 1); else r64::step16(d + N * l, 1);
+                    if constexpr (N == 8) r64::step8(d + (N + 1) * l, 1); else r64::step16(d + (N + 1) * l, 1);
                     wave_sync_lds();
                     double best = -1.0;
                     int bi = -1;
 #pragma unroll
                     for (int c = 0; c < N; c++) {
                         const int e = l * N + c;
-                        const double a = fabs(d[e]);
+                        const double a = fabs(d[l * (N + 1) + c]);
                         const bool take = e != 0 && a >= best;
                         best = take ? a : best;
                         bi = take ? e : bi;
@@ -884,8 +889,12 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
                 }
             }
             wave_sync_lds();
+            const float inv = 1.0f / (float)max(ncols, 1);
             for (int e = lane; e < nrows * ncols; e += 64) {
-                const int r = e / ncols, c = colidx[e - r * ncols];
+                int r = (int)((float)e * inv);                 // e / ncols, corrected (e < 2^12)
+                r += (r + 1) * ncols <= e;
+                r -= r * ncols > e;
+                const int c = colidx[e - r * ncols];
                 lum[r * LW + c] = luma(reinterpret_cast<const uint8_t*>(&raw[r * PDW]) + mis[r] + c * BPP);
             }
             wave_sync_lds();
@@ -994,7 +1003,7 @@ static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
     if (p.m.tile_h != FixStrip<N, SEM>::TH || p.tiles_x != (p.m.w + Geo<N, SEM>::TW - 1) / Geo<N, SEM>::TW)
         return hipErrorInvalidValue;
     const int nstrips = p.tiles_x * FixStrip<N, SEM>::SPT * ((p.m.y1 - p.m.y0 + p.m.tile_h - 1) / p.m.tile_h);
-    const int blocks = nstrips < 2048 ? nstrips : 2048;   // one wave each; ~6-8 per CU
+    const int blocks = nstrips < 4096 ? nstrips : 4096;   // one wave each; up to ~10 per CU (LDS)
     hipLaunchKernelGGL((dcte_fix_strips<N, BPP, SEM>), dim3(blocks), dim3(64), 0, s, p);
     return hipGetLastError();
 }
