@@ -75,8 +75,11 @@ def main():
                 torch.cuda.synchronize()
                 return a0.elapsed_time(a1) / a.iters
 
-            ms_map = timed(0.0)
-            ms_all = timed(4e-6)
+            # interleaved rounds, best of each (clock ramps and neighbours on the box)
+            ms_map, ms_all = 1e9, 1e9
+            for _ in range(3):
+                ms_map = min(ms_map, timed(0.0))
+                ms_all = min(ms_all, timed(4e-6))
             ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, 4e-6)
             # flagged count: the host entry point reports it (same kernels)
             host = fr.cpu().numpy()
