@@ -2,6 +2,10 @@
 the raw summaries into profiles/<round>/.
 
     python tools/pmc_summary.py gpurun_out r01 [--size 16384] [--n 8]
+        [--dirs 03_pmc 04_pmc ...] [--trace 02_trace] [--tag n8]
+
+--dirs / --trace name the tools/gpu.sh step directories under the source
+directory (default: pmc_* and prof_trace, the older layout).
 
 Counter corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE is in KiB and on
 gfx950 counts 128-B fabric reads as 64 B, so HBM read bytes = 2 x FETCH_SIZE x
@@ -36,15 +40,30 @@ def main():
     kname = f"dcte_map<{n}, 3, 0>"
     dst = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(dst, exist_ok=True)
+    def opt_list(flag):
+        if flag not in sys.argv:
+            return None
+        i = sys.argv.index(flag) + 1
+        out = []
+        while i < len(sys.argv) and not sys.argv[i].startswith("--"):
+            out.append(sys.argv[i])
+            i += 1
+        return out
+    dirs = opt_list("--dirs")
+    trace = (opt_list("--trace") or ["prof_trace"])[0]
+    tagp = (opt_list("--tag") or [""])[0]
+    tagp = tagp + "_" if tagp else ""
     counters = {}
-    for f in glob.glob(os.path.join(src, "pmc_*", "*counter_collection.csv")):
+    files = ([f for d in dirs for f in glob.glob(os.path.join(src, d, "*counter_collection.csv"))]
+             if dirs else glob.glob(os.path.join(src, "pmc_*", "*counter_collection.csv")))
+    for f in files:
         counters.update(per_dispatch(f, kname))
         tag = os.path.basename(os.path.dirname(f))
-        shutil.copy(f, os.path.join(dst, f"{tag}.csv"))
-    stats = os.path.join(src, "prof_trace", "run_kernel_stats.csv")
+        shutil.copy(f, os.path.join(dst, f"{tagp}{tag}.csv"))
+    stats = os.path.join(src, trace, "run_kernel_stats.csv")
     kern_ns = None
     if os.path.exists(stats):
-        shutil.copy(stats, os.path.join(dst, "kernel_stats.csv"))
+        shutil.copy(stats, os.path.join(dst, f"{tagp}kernel_stats.csv"))
         for r in csv.DictReader(open(stats)):
             if kname in r["Name"]:
                 kern_ns = float(r["AverageNs"])
@@ -71,7 +90,7 @@ def main():
     allsum = json.load(open(path)) if os.path.exists(path) else {}
     allsum[f"dcte_map<{n},3>@{size}"] = dict(out, round=rnd)
     json.dump(allsum, open(path, "w"), indent=1)
-    json.dump(out, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(dst, f"{tagp}pmc_summary.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 
