@@ -447,6 +447,38 @@ __device__ __forceinline__ void fix_store(const FixParams& p, const Pix& q, doub
 }
 
 // The reference transform + last-maximum scan of one window held in
+// The reference's last-maximum scan (src/dct.c:100-108) as plain maxima, no
+// index tracking: the winner is the LAST index holding M = max |C| over the
+// non-DC coefficients, and only two indices are edge atoms (src/dct.c:18-25),
+// 1 = (0,1) and N = (1,0).  With a01 = |C01|, a10 = |C10|, mb = max over
+// indices 2 .. N-1 and ma = max over indices > N (-1 for an empty set):
+//     edge  <=>  ma < M  and  (a10 == M  or  (mb < M  and  a01 == M))
+// -- exact comparisons of the very doubles the scan compares, so the class
+// is the scan's (the all-zero window: ma == M == 0, texture, as the scan).
+__device__ __forceinline__ void lastmax_decide(double a01, double a10, double mb, double ma,
+                                               double& m, bool& edge)
+{
+    m = fmax(fmax(ma, a10), fmax(mb, a01));
+    edge = !(ma == m) && (a10 == m || (!(mb == m) && a01 == m));
+}
+
+// Group form: lane l of an N-lane group holds coefficient row k1 = l in
+// v[0..N-1]; the decision is valid on the group's lane 0.
+template <int N>
+__device__ __forceinline__ void lastmax_group(const double* v, int l, double& m, bool& edge)
+{
+    double mb = -1.0;
+#pragma unroll
+    for (int k = 2; k < N; k++) mb = fmax(mb, fabs(v[k]));
+    const double v0 = fabs(v[0]), v1 = fabs(v[1]);
+    double pa = fmax(mb, v1);                      // row l from k2 = 1
+    pa = l >= 2 ? fmax(pa, v0) : (l == 1 ? pa : -1.0);   // indices > N
+#pragma unroll
+    for (int o = N / 2; o > 0; o >>= 1) pa = fmax(pa, __shfl_xor(pa, o, N));
+    const double a10 = __shfl(v0, 1, N);           // lane 1's |C10|
+    lastmax_decide(v1, a10, mb, pa, m, edge);
+}
+
 // registers (N <= 8): ddct8x8s along the first index, then the second;
 // ddct2d (N = 2, 4) the second index first.  The scan keeps the LAST maximum
 // (src/dct.c:103, "max <= currval"); edge atoms (0,1), (1,0) (src/dct.c:18-25).
@@ -472,15 +504,12 @@ __device__ __forceinline__ void refine_regs(double (&d)[N * N], const double* ct
 #pragma unroll
         for (int i = 0; i < N; i++) r64::step_small(N, d + i, N, ct);
     }
-    m = 0.0;
-    edge = false;
+    double mb = -1.0, ma = -1.0;
 #pragma unroll
-    for (int e = 1; e < N * N; e++) {
-        const double v = fabs(d[e]);
-        const bool take = m <= v;
-        m = take ? v : m;
-        edge = take ? (e == 1 || e == N) : edge;
-    }
+    for (int e = 2; e < N; e++) mb = fmax(mb, fabs(d[e]));
+#pragma unroll
+    for (int e = N + 1; e < N * N; e++) ma = fmax(ma, fabs(d[e]));
+    lastmax_decide(fabs(d[1]), fabs(d[N]), mb, ma, m, edge);
 }
 
 __device__ __forceinline__ void wave_sync_lds()
@@ -492,7 +521,7 @@ __device__ __forceinline__ void wave_sync_lds()
 
 // N = 16: the 16-lane group of lane l owns the window d[0..255] (LDS, filled
 // and made visible by the caller): ddct16x16s, then row k1 = l's last
-// maximum, then the group's (largest index wins ties).  Every lane of the
+// maximum (lastmax_group).  Every lane of the
 // wave must call it (wave barriers inside).
 __device__ __forceinline__ void refine16_group(double* d, int l, double& best, bool& edge)
 {
@@ -500,25 +529,10 @@ __device__ __forceinline__ void refine16_group(double* d, int l, double& best, b
     wave_sync_lds();
     r64::step16(d + 16 * l, 1);              // ... then the second
     wave_sync_lds();
-    best = -1.0;
-    int bi = -1;
+    double v[16];
 #pragma unroll
-    for (int c = 0; c < 16; c++) {
-        const int e = l * 16 + c;
-        const double v = fabs(d[e]);
-        const bool take = e != 0 && v >= best;
-        best = take ? v : best;
-        bi = take ? e : bi;
-    }
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) {
-        const double ob = __shfl_xor(best, o, 16);
-        const int oi = __shfl_xor(bi, o, 16);
-        const bool take = ob > best || (ob == best && oi > bi);
-        best = take ? ob : best;
-        bi = take ? oi : bi;
-    }
-    edge = bi == 1 || bi == 16;
+    for (int c = 0; c < 16; c++) v[c] = d[l * 16 + c];
+    lastmax_group<16>(v, l, best, edge);
 }
 
 template <int N, int SEM>
@@ -620,7 +634,7 @@ __device__ __forceinline__ int wave_min(int v)
 // (ddct8x8s / ddct16x16s transform along the first index for each second
 // index), the lines meet in the group's window buffer w, lane l runs the
 // second pass on coefficient row l and scans it (last maximum,
-// src/dct.c:103), and the group reduces (larger index wins ties).  `at` =
+// src/dct.c:103, as maxima: lastmax_group).  `at` =
 // the lum index of window element (0, 0); w holds N rows of N + 1 doubles
 // (the pad keeps both passes' accesses on distinct LDS banks).  Every lane
 // of the wave calls it.
@@ -640,25 +654,7 @@ __device__ __forceinline__ void refine_group(const double* lum, int LW, int at, 
     for (int k = 0; k < N; k++) v[k] = w[l * (N + 1) + k];
     wave_sync_lds();                                   // w may be refilled after this
     if constexpr (N == 8) r64::step8(v, 1); else r64::step16(v, 1);
-    best = -1.0;
-    int bi = -1;
-#pragma unroll
-    for (int k = 0; k < N; k++) {
-        const int e = l * N + k;
-        const double a = fabs(v[k]);
-        const bool take = e != 0 && a >= best;
-        best = take ? a : best;
-        bi = take ? e : bi;
-    }
-#pragma unroll
-    for (int o = N / 2; o > 0; o >>= 1) {
-        const double ob = __shfl_xor(best, o, N);
-        const int oi = __shfl_xor(bi, o, N);
-        const bool take = ob > best || (ob == best && oi > bi);
-        best = take ? ob : best;
-        bi = take ? oi : bi;
-    }
-    edge = bi == 1 || bi == N;
+    lastmax_group<N>(v, l, best, edge);
 }
 
 template <int N, int BPP, int SEM>
@@ -779,25 +775,13 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
                     wave_sync_lds();
                     if constexpr (N == 8) r64::step8(d + (N + 1) * l, 1); else r64::step16(d + (N + 1) * l, 1);
                     wave_sync_lds();
-                    double best = -1.0;
-                    int bi = -1;
+                    double v[N];
 #pragma unroll
-                    for (int c = 0; c < N; c++) {
-                        const int e = l * N + c;
-                        const double a = fabs(d[l * (N + 1) + c]);
-                        const bool take = e != 0 && a >= best;
-                        best = take ? a : best;
-                        bi = take ? e : bi;
-                    }
-#pragma unroll
-                    for (int o = N / 2; o > 0; o >>= 1) {
-                        const double ob = __shfl_xor(best, o, N);
-                        const int oi = __shfl_xor(bi, o, N);
-                        const bool take = ob > best || (ob == best && oi > bi);
-                        best = take ? ob : best;
-                        bi = take ? oi : bi;
-                    }
-                    if (valid && l == 0) store(lx, ly, best, bi == 1 || bi == N);
+                    for (int c = 0; c < N; c++) v[c] = d[l * (N + 1) + c];
+                    double best;
+                    bool edge;
+                    lastmax_group<N>(v, l, best, edge);
+                    if (valid && l == 0) store(lx, ly, best, edge);
                     wave_sync_lds();
                 }
             }
