@@ -1,0 +1,59 @@
+"""Per-rank cost of a strong-scaling step on one GPU (no exchange): a band of
+`--rows` output rows of a 16384-wide frame, launched as bench.py does at
+world > 1 (interior rows, then the N/2-1 top and N/2 bottom halo-dependent
+rows = 3 map launches) vs one launch over the band.  HIP-event timing on the
+launch stream; prints one JSON line per pattern.
+
+    python tools/band_bench.py [--rows 2048] [--n 8] [--iters 50]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "dct-carver_amd")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=2048)
+    ap.add_argument("--width", type=int, default=16384)
+    ap.add_argument("--n", type=int, default=8)
+    ap.add_argument("--iters", type=int, default=50)
+    a = ap.parse_args()
+    import torch
+    import dctenergy
+    from dctenergy import synth
+    n, W, R = a.n, a.width, a.rows
+    hl, hr = n // 2 - 1, n // 2
+    H = 8 * R                                   # a middle band of an 8-band frame
+    Y0, Y1 = 3 * R, 4 * R
+    buf = synth.natural_rows(Y0 - hl, R + hl + hr, W, 3, seed=0, device="cuda")
+    out = torch.empty((R, W), dtype=torch.float32, device="cuda")
+    s = torch.cuda.current_stream()
+    with dctenergy.Context(ngpus=1) as ctx:
+        def run(y0, y1):
+            ctx.energy_map_device(buf.data_ptr(), buf.stride(0), W, H, 3, Y0 - hl, buf.shape[0], y0, y1,
+                                  n, 0.3, 0.7, out[y0 - Y0:].data_ptr(), out.stride(0), s.cuda_stream)
+        pats = {"one launch": [(Y0, Y1)],
+                "interior + 2 edge launches (bench.py world > 1)": [(Y0 + hl, Y1 - hr), (Y0, Y0 + hl), (Y1 - hr, Y1)]}
+        for name, ranges in pats.items():
+            for _ in range(5):
+                for r in ranges:
+                    run(*r)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record(s)
+            for _ in range(a.iters):
+                for r in ranges:
+                    run(*r)
+            e1.record(s)
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / a.iters
+            print(json.dumps({"pattern": name, "rows": R, "width": W, "n": n, "ms_per_step": round(ms, 4),
+                              "mpx_s": round(R * W / ms / 1e3, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
