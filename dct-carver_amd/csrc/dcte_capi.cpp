@@ -26,7 +26,11 @@ namespace {
 constexpr double kDefaultTieTau = 4e-6;
 
 struct FixScratch {
-    unsigned* d_count = nullptr;   // [0] list length (points / seam) or dirty tiles (map), [1] refined
+    // [0] list length (points / seam), [1] refined, [2 + phase] dirty strips of
+    // the map launches (two, alternating: each map launch zeroes the other one
+    // for the next launch, so no memset is needed between launches)
+    unsigned* d_count = nullptr;
+    unsigned phase = 0;
     unsigned* d_list = nullptr;    // flagged pixels (map: per-tile regions)
     size_t cap = 0;
     unsigned* d_tiles = nullptr;   // map: per-tile counts | dirty-tile list
@@ -160,9 +164,9 @@ bool valid_sem_bpp(int sem, int bpp)
 int ensure_fix(dcte_ctx* ctx, Device& d, hipStream_t s, size_t npix, FixScratch** out)
 {
     FixScratch& f = d.fix[s];
-    if (!f.d_count) {   // [0] flagged by the current launch, [1] refined since reset
-        DCTE_HIP(ctx, hipMalloc(&f.d_count, 2 * sizeof(unsigned)));
-        DCTE_HIP(ctx, hipMemset(f.d_count, 0, 2 * sizeof(unsigned)));
+    if (!f.d_count) {
+        DCTE_HIP(ctx, hipMalloc(&f.d_count, 4 * sizeof(unsigned)));
+        DCTE_HIP(ctx, hipMemset(f.d_count, 0, 4 * sizeof(unsigned)));
     }
     if (f.cap < npix) {
         if (f.d_list) DCTE_HIP(ctx, hipFree(f.d_list));
@@ -290,7 +294,8 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     p.fix_list = f->d_list;
     p.tile_count = f->d_tiles;
     p.dirty_list = f->d_tiles + ntiles;
-    p.dirty_count = f->d_count;
+    p.dirty_count = f->d_count + 2 + f->phase;
+    p.dirty_next = f->d_count + 2 + (f->phase ^ 1u);
 
     dcte::TileFixParams q{};
     q.m = p;
@@ -298,7 +303,7 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     q.fix_total = f->d_count + 1;
     q.tiles_x = tiles_x;
 
-    DCTE_HIP(ctx, hipMemsetAsync(f->d_count, 0, sizeof(unsigned), s));
+    f->phase ^= 1u;                 // the next launch on this stream uses the other counter
     if (ctx->profile) {
         ProfEvent ev{d.id, nullptr, nullptr};
         DCTE_HIP(ctx, hipEventCreate(&ev.a));

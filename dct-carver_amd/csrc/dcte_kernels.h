@@ -33,7 +33,8 @@ struct MapParams {
     unsigned* fix_list;
     unsigned* tile_count;
     unsigned* dirty_list;
-    unsigned* dirty_count;
+    unsigned* dirty_count;   // zero when the launch starts
+    unsigned* dirty_next;    // zeroed by this launch: the next launch's dirty_count
 };
 
 // dcte_fix_strips: the map launch's own parameters plus the fp64 pieces

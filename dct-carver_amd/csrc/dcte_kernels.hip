@@ -219,6 +219,9 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
     unsigned* strip_list = p.fix_list + (size_t)strip * (size_t)(64 * p.tile_h);
     const int sx0 = x0 + 64 * sc;                    // first column of the strip
     if (tx < SPT) nflag[tx] = 0;
+    // the next launch's dirty-strip counter (stream order: nothing reads it
+    // before this launch ends)
+    if (tx == 0 && blockIdx.x == 0 && blockIdx.y == 0) *p.dirty_next = 0u;
     const bool check_ties = we != wt;                // uniform
     const bool force_all = p.tie_tau >= 1.0f;        // uniform
     const float keep = 1.0f - p.tie_tau;             // |me - mt| <= tau * hi  <=>  lo >= (1 - tau) hi
@@ -987,7 +990,7 @@ static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
     if (p.m.tile_h != FixStrip<N, SEM>::TH || p.tiles_x != (p.m.w + Geo<N, SEM>::TW - 1) / Geo<N, SEM>::TW)
         return hipErrorInvalidValue;
     const int nstrips = p.tiles_x * FixStrip<N, SEM>::SPT * ((p.m.y1 - p.m.y0 + p.m.tile_h - 1) / p.m.tile_h);
-    const int blocks = nstrips < 4096 ? nstrips : 4096;   // one wave each; up to ~10 per CU (LDS)
+    const int blocks = nstrips < 2048 ? nstrips : 2048;   // one wave each; ~8 per CU
     hipLaunchKernelGGL((dcte_fix_strips<N, BPP, SEM>), dim3(blocks), dim3(64), 0, s, p);
     return hipGetLastError();
 }
