@@ -40,6 +40,9 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--bpp", type=int, default=3)
     ap.add_argument("--sem", type=int, default=0)
+    ap.add_argument("--e2e", action="store_true",
+                    help="time whole calls (map + refinement + launch gaps) with stream events "
+                         "instead of the map launches alone")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     import torch
@@ -54,15 +57,27 @@ def main():
     same = {}
     for r in range(a.rounds):
         for p, L, h in libs:
-            for _ in range(a.iters + 1):
+            def call():
                 rc = L.dcte_energy_map_device(h, 0, frame.data_ptr(), frame.stride(0), S, S, a.bpp, 0, S,
                                               0, S, a.n, 0.3, 0.7, a.sem, out.data_ptr(), out.stride(0), stream)
                 assert rc == 0, rc
             n = ctypes.c_longlong()
             ms = ctypes.c_double()
-            L.dcte_profile_read(h, ctypes.byref(n), ctypes.byref(ms))
-            # drop the first launch of the round (warm)
-            times[p].append(ms.value / n.value)
+            if a.e2e:
+                call()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    call()
+                e1.record()
+                torch.cuda.synchronize()
+                L.dcte_profile_read(h, ctypes.byref(n), ctypes.byref(ms))
+                times[p].append(e0.elapsed_time(e1) / a.iters)
+            else:
+                for _ in range(a.iters + 1):
+                    call()
+                L.dcte_profile_read(h, ctypes.byref(n), ctypes.byref(ms))
+                times[p].append(ms.value / n.value)
             if r == 0:
                 torch.cuda.synchronize()
                 if ref is None:
@@ -70,7 +85,7 @@ def main():
                 same[p] = bool(torch.equal(out, ref))
     for p in a.libs:
         t = times[p]
-        print(json.dumps({"lib": os.path.basename(p), "n": a.n, "size": S,
+        print(json.dumps({"lib": os.path.basename(p), "n": a.n, "size": S, "e2e": a.e2e,
                           "median_ms": round(statistics.median(t), 4), "min_ms": round(min(t), 4),
                           "mpx_s": round(S * S / statistics.median(t) / 1e3, 1),
                           "bit_equal_first": same[p]}))
