@@ -796,34 +796,37 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
         // entries are a contiguous run [pos, end) of the list.
         const bool interior = sx0 - HL >= 0 && (sx0 - HL + LW) * BPP + 3 <= p.w * BPP;
         for (unsigned pos = 0; pos < cnt;) {                           // uniform
-            const int b = band_of(list[pos]);
-            // the run's end and the luma columns its windows need (bits of a 96-bit mask)
-            unsigned end = pos;
-            uint32_t m0 = 0, m1 = 0, m2 = 0;
-            for (;;) {
+            // the run's end and the luma columns its windows need (a 128-bit
+            // mask); a run of <= 64 entries stays in registers (loc0)
+            unsigned end = pos, loc0 = 0;
+            int b = 0;
+            bool single = true;
+            uint64_t mlo = 0, mhi = 0;
+            for (int chunk = 0;; chunk++) {
                 const unsigned q = end + lane;
                 const unsigned loc = q < cnt ? list[q] : 0u;
+                if (chunk == 0) {
+                    b = band_of(__shfl(loc, 0));
+                    loc0 = loc;
+                }
                 const bool in = q < cnt && band_of(loc) == b;
                 if (in) {
+                    constexpr uint64_t bits = (1ull << N) - 1;
                     const int lx = (int)(loc & 63);
-#pragma unroll
-                    for (int o = 0; o < N; o++) {
-                        const int c = lx + o;
-                        if (c < 32) m0 |= 1u << c;
-                        else if (c < 64) m1 |= 1u << (c - 32);
-                        else m2 |= 1u << (c - 64);
-                    }
+                    mlo |= bits << lx;
+                    if (lx + N > 64) mhi |= bits >> (64 - lx);
                 }
                 const int nin = __popcll(__ballot(in));     // a prefix of the lanes
                 end += nin;
                 if (nin < 64) break;
+                single = false;
             }
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) {
-                m0 |= __shfl_xor(m0, o);
-                m1 |= __shfl_xor(m1, o);
-                m2 |= __shfl_xor(m2, o);
+                mlo |= __shfl_xor(mlo, o);
+                mhi |= __shfl_xor(mhi, o);
             }
+            const uint32_t m0 = (uint32_t)mlo, m1 = (uint32_t)(mlo >> 32), m2 = (uint32_t)mhi;
             // band b: output rows [max(A, 0), min(A + SBH, ye - ys)), A = b SBH - (N - 1);
             // input rows from r0 = max(A, 0) - HL (tile-relative)
             const int A = b * SBH - (N - 1);
@@ -888,7 +891,7 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
             // element (i, j) of pixel (lx, ly): lum row ly + oy - HL - r0, column lx + ox
             if constexpr (!kGroup) {
                 for (unsigned q = pos + lane; q < end; q += 64) {
-                    const unsigned loc = list[q];
+                    const unsigned loc = single ? loc0 : list[q];
                     const int ly = (int)(loc >> 6), lx = (int)(loc & 63);
                     const double* base = &lum[(ly - HL - r0) * LW + lx];
                     double d[N * N];
@@ -910,7 +913,8 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
                 for (unsigned q0 = pos; q0 < end; q0 += PPW) {        // uniform
                     const unsigned q = q0 + grp;
                     const bool valid = q < end;
-                    const unsigned loc = valid ? list[q] : list[pos];
+                    const unsigned lq = __shfl(loc0, (int)(q - pos) & 63);
+                    const unsigned loc = single ? (valid ? lq : loc0) : list[valid ? q : pos];
                     const int ly = (int)(loc >> 6), lx = (int)(loc & 63);
                     double best;
                     bool edge;
