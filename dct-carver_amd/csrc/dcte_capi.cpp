@@ -106,6 +106,7 @@ struct dcte_ctx {
     double tie_tau = kDefaultTieTau;
     bool profile = false;
     double pin_mib = 64.0;          // DCTE_OPT_PIN_HOST
+    int tile_h = 0;                 // DCTE_OPT_TILE_H (0: the kernel's default)
     std::vector<ProfEvent> prof;
     long long last_refined = 0;
     std::string last_error;
@@ -259,13 +260,14 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     size_t npix = (size_t)(y1 - y0) * (size_t)w;
     if (npix >= (1ULL << 32)) return DCTE_ERANGE;
     // one workgroup's output rows go through one buffer resource
-    if ((long long)dcte::map_default_tile_h(n) * out_stride * 4 >= (1LL << 31)) return DCTE_ERANGE;
+    const int tile_h = ctx->tile_h > 0 ? ctx->tile_h : dcte::map_default_tile_h(n);
+    if ((long long)tile_h * out_stride * 4 >= (1LL << 31)) return DCTE_ERANGE;
 
     DCTE_HIP(ctx, hipSetDevice(d.id));
     // refinement lists: one region of 64 * tile_h entries per 64-column strip
-    const int tiles_x = dcte::map_tiles_x(n, w), tiles_y = dcte::map_tiles_y(n, y1 - y0);
+    const int tiles_x = dcte::map_tiles_x(n, w), tiles_y = dcte::map_tiles_y(n, y1 - y0, tile_h);
     const size_t ntiles = (size_t)tiles_x * (size_t)tiles_y * (size_t)dcte::map_strips_per_tile(n);
-    const size_t list_len = ntiles * 64 * (size_t)dcte::map_default_tile_h(n);
+    const size_t list_len = ntiles * 64 * (size_t)tile_h;
     if (list_len >= (1ULL << 32)) return DCTE_ERANGE;
     FixScratch* f = nullptr;
     int rc = ensure_fix(ctx, d, s, list_len, &f);
@@ -283,7 +285,7 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     p.in_rows = in_rows;
     p.y0 = y0;
     p.y1 = y1;
-    p.tile_h = dcte::map_default_tile_h(n);
+    p.tile_h = tile_h;
     p.out = d_out;
     p.out_stride = out_stride;
     p.we = (float)((double)edges / scale);
@@ -586,6 +588,10 @@ int dcte_set_option(dcte_ctx* ctx, int option, double value)
     case DCTE_OPT_PIN_HOST:
         if (!(value >= 0)) return DCTE_EINVAL;
         ctx->pin_mib = value;
+        return DCTE_OK;
+    case DCTE_OPT_TILE_H:
+        if (!(value >= 0 && value <= 4096)) return DCTE_EINVAL;
+        ctx->tile_h = (int)value;
         return DCTE_OK;
     default: return DCTE_EINVAL;
     }

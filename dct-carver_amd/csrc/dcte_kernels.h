@@ -117,7 +117,7 @@ int dp_max_tiles(int device);
 int map_tile_w(int n);
 int map_default_tile_h(int n);
 int map_tiles_x(int n, int w);                 // map grid (tiles) of a launch
-int map_tiles_y(int n, int rows);
+int map_tiles_y(int n, int rows, int tile_h);
 int map_strips_per_tile(int n);
 
 }  // namespace dcte

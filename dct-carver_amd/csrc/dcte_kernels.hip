@@ -613,7 +613,6 @@ constexpr unsigned kFixDirect = 32;
 
 template <int N, int SEM>
 struct FixStrip {
-    static constexpr int TH = N == 16 ? DCTE_TILE_H16 : DCTE_TILE_H;
     static constexpr int SPT = Lanes<N>::S == 1 ? Geo<N, SEM>::TW / 64 : 1;   // strips per tile
     static constexpr int LW = 64 + N - 1;             // luma columns of a strip
     static constexpr int G = Geo<N, SEM>::G;          // map kernel rows per group
@@ -664,7 +663,7 @@ template <int N, int BPP, int SEM>
 __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
 {
     using FS = FixStrip<N, SEM>;
-    constexpr int TH = FS::TH, SPT = FS::SPT, LW = FS::LW, G = FS::G, SBH = FS::SBH, LR = FS::LR;
+    constexpr int SPT = FS::SPT, LW = FS::LW, G = FS::G, SBH = FS::SBH, LR = FS::LR;
     constexpr int TW = Geo<N, SEM>::TW;
     constexpr int HL = Geo<N, SEM>::HL;
     constexpr int PB = ((LW * BPP + 3) & ~3) + 4;      // raw row pitch: the span + misalignment
@@ -723,8 +722,8 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
         const unsigned tile = strip / SPT;
         const int bx = (int)(tile % (unsigned)tp.tiles_x), by = (int)(tile / (unsigned)tp.tiles_x);
         const int sx0 = bx * TW + 64 * (int)(strip % SPT);
-        const int ys = p.y0 + by * TH, ye = min(ys + TH, p.y1);
-        const unsigned* list = p.fix_list + (size_t)strip * (size_t)(64 * TH);
+        const int ys = p.y0 + by * p.tile_h, ye = min(ys + p.tile_h, p.y1);
+        const unsigned* list = p.fix_list + (size_t)strip * (size_t)(64 * p.tile_h);
         if (tp.fix_total && lane == 0) atomicAdd(tp.fix_total, cnt);
         auto store = [&](int lx, int ly, double m, bool edge) {
             p.out[(long long)(ys + ly - p.y0) * p.out_stride + sx0 + lx] =
@@ -936,7 +935,7 @@ int map_tile_w(int n)
 }
 int map_default_tile_h(int n) { return n == 16 ? DCTE_TILE_H16 : DCTE_TILE_H; }
 int map_tiles_x(int n, int w) { return (w + map_tile_w(n) - 1) / map_tile_w(n); }
-int map_tiles_y(int n, int rows) { return (rows + map_default_tile_h(n) - 1) / map_default_tile_h(n); }
+int map_tiles_y(int n, int rows, int tile_h) { return (rows + tile_h - 1) / tile_h; }
 int map_strips_per_tile(int n) { return n == 16 ? 1 : map_tile_w(n) / 64; }
 
 template <int N, int BPP, int SEM>
@@ -991,7 +990,7 @@ static void launch_fix_n(const FixParams& p, hipStream_t s)
 template <int N, int BPP, int SEM>
 static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
 {
-    if (p.m.tile_h != FixStrip<N, SEM>::TH || p.tiles_x != (p.m.w + Geo<N, SEM>::TW - 1) / Geo<N, SEM>::TW)
+    if (p.m.tile_h < 1 || p.tiles_x != (p.m.w + Geo<N, SEM>::TW - 1) / Geo<N, SEM>::TW)
         return hipErrorInvalidValue;
     const int nstrips = p.tiles_x * FixStrip<N, SEM>::SPT * ((p.m.y1 - p.m.y0 + p.m.tile_h - 1) / p.m.tile_h);
     const int blocks = nstrips < 2048 ? nstrips : 2048;   // one wave each; ~8 per CU

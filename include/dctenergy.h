@@ -77,6 +77,8 @@ extern "C" {
                                are at least this many MiB (default 64; 0 = never),
                                so the chunked H2D / D2H copies overlap (pageable
                                copies are staged serially by the runtime) */
+#define DCTE_OPT_TILE_H 4   /* output rows per map workgroup (0 = the kernel's
+                               default, 128); results do not depend on it */
 
 typedef struct dcte_ctx dcte_ctx;
 

@@ -371,3 +371,18 @@ def test_multi_device_host_path_on_one_gpu(ctx, G):
             for mode, ch in ((dctenergy.DCTE_NORM_LQR, 1), (dctenergy.DCTE_NORM_PREVIEW, 3)):
                 assert np.array_equal(ctx.energy_image_u8(img, n, 0.3, 0.7, mode, ch),
                                       many.energy_image_u8(img, n, 0.3, 0.7, mode, ch)), (n, mode)
+
+
+@pytest.mark.parametrize("n", [2, 4, 8, 16])
+def test_tile_height_does_not_change_results(n):
+    """DCTE_OPT_TILE_H only re-partitions the work: any tile height gives the
+    bit-identical map, refinement included (tie-dense input, e != t)."""
+    rng = np.random.default_rng(n)
+    img = np.where(rng.random((301, 333)) < 1 / 40, 255, 16).astype(np.uint8)
+    img3 = rng.integers(0, 256, (150, 257, 3), dtype=np.uint8)
+    with dctenergy.Context(ngpus=1) as c:
+        ref = [c.energy_map(x, n, 0.3, 0.7) for x in (img, img3)]
+        for th in (1, 7, 32, 64, 200):
+            c.set_option(dctenergy.DCTE_OPT_TILE_H, th)
+            for x, r in zip((img, img3), ref):
+                assert np.array_equal(c.energy_map(x, n, 0.3, 0.7), r), (n, th)

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--width", type=int, default=16384)
     ap.add_argument("--n", type=int, default=8)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--tile-h", type=int, default=0)
     a = ap.parse_args()
     import torch
     import dctenergy
@@ -33,6 +34,8 @@ def main():
     out = torch.empty((R, W), dtype=torch.float32, device="cuda")
     s = torch.cuda.current_stream()
     with dctenergy.Context(ngpus=1) as ctx:
+        ctx.set_option(dctenergy.DCTE_OPT_TILE_H, a.tile_h)
+
         def run(y0, y1):
             ctx.energy_map_device(buf.data_ptr(), buf.stride(0), W, H, 3, Y0 - hl, buf.shape[0], y0, y1,
                                   n, 0.3, 0.7, out[y0 - Y0:].data_ptr(), out.stride(0), s.cuda_stream)
@@ -51,7 +54,8 @@ def main():
             e1.record(s)
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / a.iters
-            print(json.dumps({"pattern": name, "rows": R, "width": W, "n": n, "ms_per_step": round(ms, 4),
+            print(json.dumps({"pattern": name, "rows": R, "width": W, "n": n, "tile_h": a.tile_h,
+                              "ms_per_step": round(ms, 4),
                               "mpx_s": round(R * W / ms / 1e3, 1)}), flush=True)
 
 
