@@ -260,7 +260,15 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     size_t npix = (size_t)(y1 - y0) * (size_t)w;
     if (npix >= (1ULL << 32)) return DCTE_ERANGE;
     // one workgroup's output rows go through one buffer resource
-    const int tile_h = ctx->tile_h > 0 ? ctx->tile_h : dcte::map_default_tile_h(n);
+    // default tile height; a launch that would fill the chip only about once
+    // (a strong-scaling rank's 2048-row band: 1024 workgroups) uses half-height
+    // tiles, whose second round evens out the finish (−3.5 % per band,
+    // tools/band_bench.py, profiles/r02/band_tile_h.jsonl)
+    int tile_h = ctx->tile_h > 0 ? ctx->tile_h : dcte::map_default_tile_h(n);
+    if (ctx->tile_h <= 0 && n == 8 &&
+        (long long)dcte::map_tiles_x(n, w) * dcte::map_tiles_y(n, y1 - y0, tile_h) < 2048 &&
+        y1 - y0 >= 1024)
+        tile_h /= 2;
     if ((long long)tile_h * out_stride * 4 >= (1LL << 31)) return DCTE_ERANGE;
 
     DCTE_HIP(ctx, hipSetDevice(d.id));
