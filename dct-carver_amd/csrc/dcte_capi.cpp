@@ -762,6 +762,57 @@ int dcte_energy_points(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, 
     return sync_bands(ctx, 1);
 }
 
+int dcte_energy_windows_device(dcte_ctx* ctx, int device, const double* d_win, int count, int n,
+                               float edges, float textures, float* d_out, void* stream)
+{
+    DeviceGuard guard_;
+    if (!ctx) return DCTE_EINVAL;
+    DCTE_ARG(ctx, device >= 0 && device < (int)ctx->devs.size());
+    DCTE_ARG(ctx, valid_n(n) && count >= 0);
+    if (count == 0) return DCTE_OK;
+    DCTE_ARG(ctx, d_win && d_out);
+    DCTE_HIP(ctx, hipSetDevice(ctx->devs[device].id));
+    dcte::WinParams p{};
+    p.win = d_win;
+    p.count = count;
+    p.n = n;
+    small_twiddles(n, p.ct);
+    p.edges = edges;
+    p.textures = textures;
+    p.out = d_out;
+    DCTE_HIP(ctx, dcte::launch_windows(p, (hipStream_t)stream));
+    return DCTE_OK;
+}
+
+int dcte_energy_windows(dcte_ctx* ctx, const double* win, int count, int n, float edges,
+                        float textures, float* out)
+{
+    DeviceGuard guard_;
+    if (!ctx) return DCTE_EINVAL;
+    DCTE_ARG(ctx, valid_n(n) && count >= 0);
+    if (count == 0) return DCTE_OK;
+    DCTE_ARG(ctx, win && out);
+    Device& d = ctx->devs[0];
+    int rc = ensure_stream(ctx, d);
+    if (rc) return rc;
+    const size_t wbytes = sizeof(double) * (size_t)n * n * (size_t)count;
+    rc = ensure_buf(ctx, (void**)&d.d_in, &d.in_cap, wbytes);
+    if (rc) return rc;
+    rc = ensure_buf(ctx, (void**)&d.d_out, &d.out_cap, sizeof(float) * (size_t)count);
+    if (rc) return rc;
+    DCTE_HIP(ctx, hipMemcpyAsync(d.d_in, win, wbytes, hipMemcpyHostToDevice, d.stream));
+    rc = dcte_energy_windows_device(ctx, 0, reinterpret_cast<const double*>(d.d_in), count, n, edges,
+                                    textures, d.d_out, d.stream);
+    if (rc) {
+        drain(ctx, 1);
+        return rc;
+    }
+    DCTE_HIP(ctx, hipMemcpyAsync(out, d.d_out, sizeof(float) * (size_t)count, hipMemcpyDeviceToHost,
+                                 d.stream));
+    DCTE_HIP(ctx, hipStreamSynchronize(d.stream));
+    return DCTE_OK;
+}
+
 int dcte_seam_find_device(dcte_ctx* ctx, int device, const float* d_map, long long map_stride,
                           int w, int h, int* d_seam, void* stream)
 {

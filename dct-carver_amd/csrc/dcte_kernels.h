@@ -83,6 +83,16 @@ struct SeamParams {
     unsigned fix_cap;
 };
 
+// Energies of given windows (dcte_windows): count windows of N x N doubles,
+// the reference's data[i][j] layout, in the reference's arithmetic.
+struct WinParams {
+    const double* win;
+    int count, n;
+    double ct[4];            // makect twiddles (N = 2, 4)
+    float edges, textures;
+    float* out;
+};
+
 // Minimum-energy seam (dcte_dp.hip): scratch sized by the launcher.
 struct DpParams {
     const float* map;        // w x h energies
@@ -107,6 +117,7 @@ hipError_t launch_fix(const FixParams& p, hipStream_t s);
 hipError_t launch_fix_tiles(int n, int bpp, int sem, const TileFixParams& p, hipStream_t s);
 hipError_t launch_seam_carve(const SeamParams& p, hipStream_t s);
 hipError_t launch_points(const SeamParams& p, hipStream_t s);
+hipError_t launch_windows(const WinParams& p, hipStream_t s);
 hipError_t launch_seam_find(const DpParams& p, hipStream_t s);
 int dp_tile_cols();
 int dp_band_rows();

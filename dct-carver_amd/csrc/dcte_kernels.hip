@@ -927,6 +927,50 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
     }
 }
 
+// ------------------------------------------------------------------ windows
+// dctNxN + weighted_max_dct_correlation (src/dct.c:77-110) on windows the
+// caller filled -- the per-window form of the callback (src/render.c:146-155
+// fills data[dx][dy] and calls exactly these two) -- in fp64 in the
+// reference's operation order: bit-identical to the reference.  One lane per
+// window for N <= 8 (registers), one 16-lane group for N = 16 (LDS).
+template <int N>
+__global__ __launch_bounds__(kFixThreads) void dcte_windows(const WinParams p)
+{
+    __shared__ double win[N == 16 ? kFixThreads / 16 : 1][N == 16 ? 256 : 1];
+    if constexpr (N <= 8) {
+        for (long long k = blockIdx.x * (long long)kFixThreads + threadIdx.x; k < p.count;
+             k += (long long)gridDim.x * kFixThreads) {
+            const double* src = p.win + k * (N * N);
+            double d[N * N];
+#pragma unroll
+            for (int e = 0; e < N * N; e++) d[e] = src[e];
+            double m;
+            bool edge;
+            refine_regs<N>(d, p.ct, m, edge);
+            p.out[k] = edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
+        }
+    } else {
+        const int l = threadIdx.x & 15, slot = threadIdx.x >> 4;
+        double* d = win[slot];
+        const long long per_pass = (long long)gridDim.x * (kFixThreads / 16);
+        const long long rounds = (p.count + per_pass - 1) / per_pass;   // uniform
+        for (long long r = 0; r < rounds; r++) {
+            const long long k = r * per_pass + blockIdx.x * (kFixThreads / 16) + slot;
+            const bool valid = k < p.count;
+            if (valid) {
+#pragma unroll
+                for (int t = 0; t < 16; t++) d[t * 16 + l] = p.win[k * 256 + t * 16 + l];
+            }
+            wave_sync_lds();
+            double m;
+            bool edge;
+            refine16_group(d, l, m, edge);
+            if (valid && l == 0) p.out[k] = edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
+            wave_sync_lds();
+        }
+    }
+}
+
 // ------------------------------------------------------------------ launchers
 int map_tile_w(int n)
 {
@@ -1022,6 +1066,22 @@ hipError_t launch_fix_tiles(int n, int bpp, int sem, const TileFixParams& p, hip
     case 16: return launch_fix_tiles_n<16>(bpp, sem, p, s);
     default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_windows(const WinParams& p, hipStream_t s)
+{
+    if (p.count <= 0) return hipSuccess;
+    const long long per_block = p.n == 16 ? kFixThreads / 16 : kFixThreads;
+    const long long want = (p.count + per_block - 1) / per_block;
+    const dim3 grid((unsigned)(want < 2048 ? want : 2048)), block(kFixThreads);
+    switch (p.n) {
+    case 2: hipLaunchKernelGGL((dcte_windows<2>), grid, block, 0, s, p); break;
+    case 4: hipLaunchKernelGGL((dcte_windows<4>), grid, block, 0, s, p); break;
+    case 8: hipLaunchKernelGGL((dcte_windows<8>), grid, block, 0, s, p); break;
+    case 16: hipLaunchKernelGGL((dcte_windows<16>), grid, block, 0, s, p); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_fix(const FixParams& p, hipStream_t s)

@@ -44,7 +44,7 @@ EXPORTS = ("dcte_abi_version", "dcte_device_count", "dcte_create", "dcte_destroy
            "dcte_last_error", "dcte_normalize_u8", "dcte_energy_image_u8", "dcte_minmax_device",
            "dcte_normalize_u8_device", "dcte_seam_carve_device", "dcte_energy_points",
            "dcte_energy_points_device", "dcte_seam_find_device", "dcte_seam_find",
-           "dcte_carve")
+           "dcte_carve", "dcte_energy_windows", "dcte_energy_windows_device")
 
 _lib = None
 
@@ -132,6 +132,10 @@ def lib():
     L.dcte_energy_points.argtypes = [vp, vp, i, i, i, ctypes.c_size_t, vp, i, i, f, f, i, vp]
     L.dcte_energy_points_device.restype = i
     L.dcte_energy_points_device.argtypes = [vp, i, vp, ll, i, i, i, vp, i, i, f, f, i, vp, vp]
+    L.dcte_energy_windows.restype = i
+    L.dcte_energy_windows.argtypes = [vp, vp, i, i, f, f, vp]
+    L.dcte_energy_windows_device.restype = i
+    L.dcte_energy_windows_device.argtypes = [vp, i, vp, i, i, f, f, vp, vp]
     L.dcte_seam_find_device.restype = i
     L.dcte_seam_find_device.argtypes = [vp, i, vp, ll, i, i, vp, vp]
     L.dcte_seam_find.restype = i
@@ -357,6 +361,19 @@ class Context:
             ctypes.c_void_p(emap_out.data_ptr()), emap_out.stride(0), n, edges, textures,
             semantics, ctypes.c_void_p(stream)))
         return px_out, emap_out
+
+    # -- per-window energies (SURVEY §8b dcte_energy_window, batched)
+    def energy_windows(self, win, edges=0.5, textures=0.5):
+        """win: K x N x N float64 windows in the reference's data[i][j]
+        layout (i = x offset for the liblqr callback) -> K float32 energies,
+        bit-identical to weighted_max_dct_correlation(dctNxN(window))."""
+        win = np.ascontiguousarray(win, dtype=np.float64)
+        if win.ndim != 3 or win.shape[1] != win.shape[2]:
+            raise ValueError("win must be K x N x N")
+        out = np.empty(win.shape[0], np.float32)
+        self._check(lib().dcte_energy_windows(self._h, win.ctypes.data, win.shape[0], win.shape[1],
+                                              edges, textures, out.ctypes.data))
+        return out
 
     # -- minimum-energy seam (SURVEY §8f-4)
     def seam_find(self, E):

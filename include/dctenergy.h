@@ -173,6 +173,21 @@ int dcte_energy_points_device(dcte_ctx *ctx, int device, const void *d_px, long 
                               float edges, float textures, int semantics, float *d_out,
                               void *stream);
 
+/* Energies of windows the caller filled (SURVEY §8b dcte_energy_window, in
+ * batches): win = count windows of n*n doubles in the reference's data[i][j]
+ * layout -- what dct_pixel_energy gathers (src/render.c:146-152: i = x
+ * offset, j = y offset, luma in [0, 1]) -- and out[k] = the
+ * weighted_max_dct_correlation of dctNxN of window k (src/dct.c:77-110),
+ * computed in fp64 in the reference's operation order on the device:
+ * bit-identical to the reference for any input.  For a liblqr-side hook that
+ * keeps its own reading windows (seam updates after the carver shrank).
+ * Host version: windows copied to the first device; device version:
+ * stream-ordered. */
+int dcte_energy_windows(dcte_ctx *ctx, const double *win, int count, int n, float edges,
+                        float textures, float *out);
+int dcte_energy_windows_device(dcte_ctx *ctx, int device, const double *d_win, int count, int n,
+                               float edges, float textures, float *d_out, void *stream);
+
 /* ---- minimum-energy seam ---------------------------------
  * liblqr's cumulative energy for the reference's carver configuration
  * (lqr_carver_init(carver, 1, 0), src/render.c:313: delta_x 1, rigidity 0)

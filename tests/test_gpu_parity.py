@@ -386,3 +386,27 @@ def test_tile_height_does_not_change_results(n):
             c.set_option(dctenergy.DCTE_OPT_TILE_H, th)
             for x, r in zip((img, img3), ref):
                 assert np.array_equal(c.energy_map(x, n, 0.3, 0.7), r), (n, th)
+
+
+def test_energy_windows_kat(ctx):
+    """dcte_energy_windows on the golden known-answer windows (the
+    reference's own transforms produced the energies): bit-exact."""
+    from golden_util import load_kat
+    for k in manifest()["kat"]:
+        win = load_kat(k["window"])
+        got = ctx.energy_windows(win[None], k["edges"], k["textures"])[0]
+        assert got == np.float32(k["energy"]), k
+
+
+@pytest.mark.parametrize("n", [2, 4, 8, 16])
+def test_energy_windows_bit_exact(ctx, n):
+    """Random, luma-quantised and tie-prone windows: bit-identical to the
+    oracle (pinned bit-exactly to the reference transforms, test_oracle.py)."""
+    rng = np.random.default_rng(40 + n)
+    wins = [rng.random((200, n, n)),
+            O.luma_plane(rng.integers(0, 256, (200, n, n, 3), dtype=np.uint8)),
+            (rng.random((200, n, n)) < 0.05) * (254 / 255) + 1 / 255]
+    for w in wins:
+        got = ctx.energy_windows(w, 0.3, 0.7)
+        ref = np.array([O.window_energy(x, 0.3, 0.7) for x in w], np.float32)
+        assert np.array_equal(got, ref), n
