@@ -410,3 +410,25 @@ def test_energy_windows_bit_exact(ctx, n):
         got = ctx.energy_windows(w, 0.3, 0.7)
         ref = np.array([O.window_energy(x, 0.3, 0.7) for x in w], np.float32)
         assert np.array_equal(got, ref), n
+
+
+@pytest.mark.parametrize("n", [2, 4, 8, 16])
+def test_refine_all_bit_exact_every_layout(n):
+    """tie_tau >= 1 sends every pixel through dcte_fix_strips (dense strips:
+    staged bands; the frame-border strips: clamped staging; small frames:
+    direct gathers): the map must equal the oracle bit for bit -- liblqr
+    grey/RGB and preview grey/RGB/RGBA, odd sizes, several tile heights."""
+    rng = np.random.default_rng(70 + n)
+    frames = [rng.integers(0, 256, (97, 131), dtype=np.uint8),
+              rng.integers(0, 256, (70, 301, 3), dtype=np.uint8),
+              rng.integers(0, 256, (41, 67, 4), dtype=np.uint8)]
+    with dctenergy.Context(ngpus=1, tie_tau=1.0) as c:
+        for th in (0, 16):
+            c.set_option(dctenergy.DCTE_OPT_TILE_H, th)
+            for img in frames:
+                if img.ndim == 2 or img.shape[2] == 3:
+                    got = c.energy_map(img, n, 0.3, 0.7)
+                    assert np.array_equal(got, O.energy_map(img, n, 0.3, 0.7)), (n, th, img.shape)
+                    assert c.last_refined == img.shape[0] * img.shape[1]
+                got = c.energy_map(img, n, 0.3, 0.7, semantics=dctenergy.DCTE_PREVIEW)
+                assert np.array_equal(got, O.preview_map(img, n, 0.3, 0.7)), (n, th, img.shape, "preview")
