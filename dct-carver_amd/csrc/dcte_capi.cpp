@@ -380,8 +380,14 @@ struct HostPin {
     HostPin& operator=(const HostPin&) = delete;
 };
 
-constexpr int kChunkRows = 2048;   // host path: output rows per pipeline chunk
-constexpr int kMaxChunks = 16;
+#ifndef DCTE_CHUNK_ROWS
+#define DCTE_CHUNK_ROWS 2048
+#endif
+#ifndef DCTE_MAX_CHUNKS
+#define DCTE_MAX_CHUNKS 16
+#endif
+constexpr int kChunkRows = DCTE_CHUNK_ROWS;   // host path: output rows per pipeline chunk
+constexpr int kMaxChunks = DCTE_MAX_CHUNKS;
 
 int ensure_pipe(dcte_ctx* ctx, Device& d, size_t nev)
 {

@@ -33,7 +33,11 @@ def main():
     ap.add_argument("--size", type=int, default=16384)
     ap.add_argument("--n", type=int, default=8)
     ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--lib", default=None, help="libdctenergy_hip.so to load (A/B)")
+    ap.add_argument("--quick", action="store_true", help="only the default host->host case")
     a = ap.parse_args()
+    if a.lib:
+        os.environ["DCTE_LIB"] = os.path.abspath(a.lib)
     import numpy as np
     import torch
     import dctenergy
@@ -52,12 +56,20 @@ def main():
         cases = (("pageable, DCTE_OPT_PIN_HOST=0 (runtime-staged copies)", px_np, out_np, 0),
                  ("pageable, page-locked per call (default)", px_np, out_np, 64),
                  ("caller-pinned buffers", px_pin.numpy(), out_pin.numpy(), 64))
+        if a.quick:
+            cases = cases[1:2]
         for name, src, dst, pin in cases:
             ctx.set_option(dctenergy.DCTE_OPT_PIN_HOST, pin)
             med, best = timed(lambda: ctx.energy_map(src, a.n, 0.3, 0.7, out=dst), a.iters)
-            res.append({"case": f"dcte_energy_map host->host ({name})", "ms": round(med * 1e3, 2),
+            res.append({"case": f"dcte_energy_map host->host ({name})", "lib": os.path.basename(dctenergy.LIB_PATH),
+                        "ms": round(med * 1e3, 2),
                         "best_ms": round(best * 1e3, 2), "mpx_s": round(mpx / med, 1)})
         ctx.set_option(dctenergy.DCTE_OPT_PIN_HOST, 64)
+        if a.quick:
+            for r in res:
+                r.update({"size": S, "n": a.n})
+                print(json.dumps(r), flush=True)
+            return
         med, best = timed(lambda: ctx.energy_image_u8(px_np, a.n, 0.3, 0.7), a.iters)
         res.append({"case": "dcte_energy_image_u8 host->host (pageable, fresh output array per call)",
                     "ms": round(med * 1e3, 2),
