@@ -177,7 +177,7 @@ def host_path(ctx, frame_dev, n, e, t, iters=3):
             "best_ms": round(ts[0] * 1e3, 2), "iters": iters,
             "bytes_h2d": int(px.nbytes), "bytes_d2h": int(out.nbytes),
             "what": f"{H}x{W} RGB pageable host frame -> dcte_energy_map -> host map "
-                    f"(PCIe-inclusive; page-locked per call, 2048-row chunk pipeline)"}
+                    f"(PCIe-inclusive; page-locked per call, 1024-row chunk pipeline)"}
 
 
 def pmc_figures(n, W, px_per_rank):

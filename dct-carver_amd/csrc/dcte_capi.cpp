@@ -381,7 +381,7 @@ struct HostPin {
 };
 
 #ifndef DCTE_CHUNK_ROWS
-#define DCTE_CHUNK_ROWS 2048
+#define DCTE_CHUNK_ROWS 1024   // A/B: 22.4 ms per 16384^2 RGB frame vs 23.1 at 2048 (profiles/r02/host_chunks.jsonl)
 #endif
 #ifndef DCTE_MAX_CHUNKS
 #define DCTE_MAX_CHUNKS 16
