@@ -43,3 +43,16 @@ def test_self_launch_weak():
 def test_single_rank():
     res = _run("--size", "33")
     assert res["n_gpus"] == 1 and res["rows_per_rank"] == [33]
+
+
+def test_failing_rank_fails_the_launch():
+    """A rank that dies (here: a band too small for the window, which
+    dctenergy.dist rejects) makes the launcher stop the others and exit
+    non-zero instead of hanging in the rendezvous or a collective."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu-rehearsal",
+                        "--gpus", "4", "--n", "16", "--size", "20"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode != 0
+    assert "needs >=" in r.stderr
