@@ -107,6 +107,7 @@ struct dcte_ctx {
     bool profile = false;
     double pin_mib = 64.0;          // DCTE_OPT_PIN_HOST
     int tile_h = 0;                 // DCTE_OPT_TILE_H (0: the kernel's default)
+    bool dp_bandwise = false;       // DCTE_OPT_DP_BANDWISE
     std::vector<ProfEvent> prof;
     long long last_refined = 0;
     std::string last_error;
@@ -607,6 +608,9 @@ int dcte_set_option(dcte_ctx* ctx, int option, double value)
         if (!(value >= 0 && value <= 4096)) return DCTE_EINVAL;
         ctx->tile_h = (int)value;
         return DCTE_OK;
+    case DCTE_OPT_DP_BANDWISE:
+        ctx->dp_bandwise = value != 0;
+        return DCTE_OK;
     default: return DCTE_EINVAL;
     }
 }
@@ -819,6 +823,17 @@ int dcte_energy_windows(dcte_ctx* ctx, const double* win, int count, int n, floa
     return DCTE_OK;
 }
 
+// A resident-mode seam search that timed out (tiles of the launch were not all
+// scheduled: other work held the CUs) switches this stream to one launch per
+// band for good; true if that is a change, i.e. worth running again.
+static bool dp_fall_back(Device& d, hipStream_t s)
+{
+    auto it = d.dp.find(s);
+    if (it == d.dp.end() || it->second.max_tiles == 0) return false;
+    it->second.max_tiles = 0;
+    return true;
+}
+
 int dcte_seam_find_device(dcte_ctx* ctx, int device, const float* d_map, long long map_stride,
                           int w, int h, int* d_seam, void* stream)
 {
@@ -841,10 +856,9 @@ int dcte_seam_find_device(dcte_ctx* ctx, int device, const float* d_map, long lo
     p.pw = (long long)p.ntiles * T;
     DpScratch& sc = d.dp[s];
     if (sc.max_tiles < 0) sc.max_tiles = dcte::dp_max_tiles(d.id);
-    if (p.ntiles > sc.max_tiles) {
-        ctx->last_error = "seam search: frame too wide for one resident DP tile per column block";
-        return DCTE_EINVAL;
-    }
+    // all tiles resident: one launch; otherwise (a frame wider than the chip
+    // holds tiles, or DCTE_OPT_DP_BANDWISE) one launch per band of rows
+    const bool resident = p.ntiles <= sc.max_tiles && !ctx->dp_bandwise;
     // scratch: jump | sjump | sx | bx | err; xch apart
     const size_t PW = (size_t)p.pw;
     const size_t n_x = (size_t)p.nb * PW, n_jump = (size_t)p.nb * PW, n_sj = (size_t)p.ns * PW;
@@ -880,7 +894,7 @@ int dcte_seam_find_device(dcte_ctx* ctx, int device, const float* d_map, long lo
     p.err = reinterpret_cast<unsigned*>(p.bx + p.nb);
     p.seam = d_seam;
     DCTE_HIP(ctx, hipMemsetAsync(p.err, 0, sizeof(unsigned), s));
-    DCTE_HIP(ctx, dcte::launch_seam_find(p, s));
+    DCTE_HIP(ctx, dcte::launch_seam_find(p, s, resident));
     return DCTE_OK;
 }
 
@@ -906,6 +920,7 @@ int dcte_seam_find(dcte_ctx* ctx, const float* map, int w, int h, int* seam)
                                  d.stream));
     DCTE_HIP(ctx, hipStreamSynchronize(d.stream));
     if (h > 0 && seam[0] < 0) {
+        if (dp_fall_back(d, d.stream)) return dcte_seam_find(ctx, map, w, h, seam);
         ctx->last_error = "seam search timed out waiting for a neighbour tile";
         return DCTE_EHIP;
     }
@@ -992,6 +1007,9 @@ int dcte_carve(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t r
     if (rc) return rc;
     for (int k = 0; k < seams; k++)
         if (hs[(size_t)k * H] < 0) {
+            if (dp_fall_back(d, s))   // the input is still on the host: carve again
+                return dcte_carve(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics,
+                                  seams, transposed, out, seam_cols);
             ctx->last_error = "seam search timed out waiting for a neighbour tile";
             return DCTE_EHIP;
         }

@@ -209,13 +209,24 @@ void dcte_seam_dp(const DpParams p)
         }
     };
 
-    // row 0 seeds M; bands j = 0 .. nb - 1 cover rows [1 + j kDpR, 1 + (j + 1) kDpR)
-    {
+    // row 0 seeds M; bands j = 0 .. nb - 1 cover rows [1 + j kDpR, 1 + (j + 1) kDpR).
+    // A launch that starts at band j0 > 0 takes row 1 + j0 kDpR - 1 from band
+    // j0 - 1's published words (every column: an earlier launch wrote them).
+    const int jb = p.j0, je = p.j1;
+    if (jb == 0) {
         float e0[C];
         set_map(0);
         load_row(e0, 0);
 #pragma unroll
         for (int c = 0; c < C; c++) { m[c] = e0[c]; s[c] = xa + c; }
+    } else {
+        const unsigned long long* xo = p.xch + (long long)(jb - 1) * pw;
+#pragma unroll
+        for (int c = 0; c < C; c++) {
+            m[c] = __int_as_float((int)(unsigned)__hip_atomic_load(xo + (xoff[c] >> 2), __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_AGENT));
+            s[c] = xa + c;
+        }
     }
     // ring of kDpNB chunks of kDpQ rows: chunk i + kDpNB - 1 is loaded while
     // chunk i runs.  A band's body is straight-line code, so the compiler
@@ -223,14 +234,15 @@ void dcte_seam_dp(const DpParams p)
     // to waiting for everything).
     constexpr int kCh = kDpR / kDpQ;                 // chunks per band
     float ring[kDpNB][kDpQ][C];
+    const int ystart = min(1 + jb * kDpR, h - 1);
+    set_map(ystart);
 #pragma unroll
     for (int i = 0; i < kDpNB - 1; i++)
 #pragma unroll
-        for (int r = 0; r < kDpQ; r++) load_row(ring[i][r], 1 + i * kDpQ + r);
-    set_map(min(1, h - 1));
-    for (int j = 0; j < p.nb; j++) {
+        for (int r = 0; r < kDpQ; r++) load_row(ring[i][r], i * kDpQ + r);
+    for (int j = jb; j < je; j++) {
         const int y0 = 1 + j * kDpR;
-        if (j > 0) {
+        if (j > jb) {
             publish(j - 1);
             if (!take_halo(j)) return;
 #pragma unroll
@@ -258,8 +270,8 @@ void dcte_seam_dp(const DpParams p)
         }
         if (y0 + kDpR < h) set_map(y0 + kDpR);       // the ring already holds its first rows
     }
-    // the last band's row is where the walk starts
-    publish(p.nb - 1);
+    // the last band's row: where the walk starts, or the next launch's seed
+    publish(je - 1);
 }
 
 __global__ __launch_bounds__(256) void dcte_seam_sjump(const DpParams p)
@@ -414,11 +426,26 @@ __global__ __launch_bounds__(kDpLanes) void dcte_seam_rows(const DpParams p)
     }
 }
 
-hipError_t launch_seam_find(const DpParams& p, hipStream_t s)
+hipError_t launch_seam_find(const DpParams& p, hipStream_t s, bool resident)
 {
     if (p.w < 1 || p.h < 1 || p.pw < (long long)p.ntiles * kDpT) return hipErrorInvalidValue;
     const int per = (p.ntiles + kXcds - 1) / kXcds;
-    hipLaunchKernelGGL(dcte_seam_dp, dim3(per * kXcds), dim3(kDpLanes), 0, s, p);
+    if (resident) {
+        // every tile resident at once: one launch, neighbours hand off in HBM
+        DpParams q = p;
+        q.j0 = 0;
+        q.j1 = p.nb;
+        hipLaunchKernelGGL(dcte_seam_dp, dim3(per * kXcds), dim3(kDpLanes), 0, s, q);
+    } else {
+        // one launch per band: a tile never waits for another in its launch
+        // (the kernel boundary orders the hand-off), so no residency is assumed
+        for (int j = 0; j < p.nb; j++) {
+            DpParams q = p;
+            q.j0 = j;
+            q.j1 = j + 1;
+            hipLaunchKernelGGL(dcte_seam_dp, dim3(per * kXcds), dim3(kDpLanes), 0, s, q);
+        }
+    }
     hipLaunchKernelGGL(dcte_seam_sjump, dim3((p.w + 255) / 256, p.ns), dim3(256), 0, s, p);
     hipLaunchKernelGGL(dcte_seam_walk, dim3(1), dim3(kWalkThreads), 0, s, p);
     hipLaunchKernelGGL(dcte_seam_rows, dim3(p.nb), dim3(kDpLanes), 0, s, p);

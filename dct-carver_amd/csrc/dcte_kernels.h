@@ -109,6 +109,9 @@ struct DpParams {
     int* bx;                 // nb
     unsigned* err;           // 1, zeroed before the launch
     int* seam;               // h: column removed per row (-1 everywhere on failure)
+    int j0, j1;              // dcte_seam_dp: bands [j0, j1) in this launch; j0 > 0 starts
+                             // from band j0 - 1's published row (launched one band at a
+                             // time when not every tile can be resident)
 };
 
 // host-side launchers (dcte_kernels.hip)
@@ -118,7 +121,7 @@ hipError_t launch_fix_tiles(int n, int bpp, int sem, const TileFixParams& p, hip
 hipError_t launch_seam_carve(const SeamParams& p, hipStream_t s);
 hipError_t launch_points(const SeamParams& p, hipStream_t s);
 hipError_t launch_windows(const WinParams& p, hipStream_t s);
-hipError_t launch_seam_find(const DpParams& p, hipStream_t s);
+hipError_t launch_seam_find(const DpParams& p, hipStream_t s, bool resident);
 int dp_tile_cols();
 int dp_band_rows();
 int dp_super_bands();

@@ -79,6 +79,10 @@ extern "C" {
                                copies are staged serially by the runtime) */
 #define DCTE_OPT_TILE_H 4   /* output rows per map workgroup (0 = the kernel's
                                default, 128); results do not depend on it */
+#define DCTE_OPT_DP_BANDWISE 5 /* 1 = run the seam search one launch per band of
+                               rows even when every DP tile fits on the chip
+                               (the mode frames wider than that use; no tile
+                               then waits on another); same seams */
 
 typedef struct dcte_ctx dcte_ctx;
 

@@ -52,6 +52,43 @@ def test_seam_device_strided_and_large(ctx):
     assert np.array_equal(seam.cpu().numpy(), O.seam_find(E))
 
 
+@pytest.fixture
+def bandwise(ctx):
+    """DCTE_OPT_DP_BANDWISE: one DP launch per band of rows (the mode a frame
+    too wide for every tile to be resident, or a timed-out search, uses)."""
+    ctx.set_option(dctenergy.DCTE_OPT_DP_BANDWISE, 1)
+    yield ctx
+    ctx.set_option(dctenergy.DCTE_OPT_DP_BANDWISE, 0)
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: f"{s[0]}x{s[1]}")
+@pytest.mark.parametrize("kind", ["ties", "valley"])
+def test_seam_bandwise_matches_oracle(bandwise, shape, kind):
+    h, w = shape
+    E = _maps(h, w, kind, h * 5 + w)
+    assert np.array_equal(bandwise.seam_find(E), O.seam_find(E))
+
+
+def test_seam_wider_than_resident_tiles(ctx):
+    """100000 columns is more DP tiles than the chip holds at once: the search
+    runs band by band instead of being refused."""
+    h, w = 200, 100000
+    E = _maps(h, w, "valley", 3)
+    E[:, 65000:65010] *= 0.01          # the valley's exit is past the old width limit
+    assert np.array_equal(ctx.seam_find(E), O.seam_find(E))
+
+
+def test_carve_bandwise_equals_resident(ctx):
+    img = load_input("natural_rgb_97x41.npy")
+    ref, ref_cols = ctx.carve(img, 12, 8, 0.5, 0.5)
+    ctx.set_option(dctenergy.DCTE_OPT_DP_BANDWISE, 1)
+    try:
+        out, cols = ctx.carve(img, 12, 8, 0.5, 0.5)
+    finally:
+        ctx.set_option(dctenergy.DCTE_OPT_DP_BANDWISE, 0)
+    assert np.array_equal(out, ref) and np.array_equal(cols, ref_cols)
+
+
 def test_seam_bad_arguments(ctx):
     L = dctenergy.lib()
     seam = np.empty(4, np.int32)

@@ -2,7 +2,7 @@
 composition + walk), map resident in HBM; checks the seam against the CPU
 restatement on a sampled case.
 
-    python tools/dp_bench.py --size 16384 --reps 10 [--lib path.so]
+    python tools/dp_bench.py --size 16384 --reps 10 [--lib path.so] [--bandwise]
 """
 import argparse
 import json
@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--lib", default="")
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--bandwise", action="store_true", help="DCTE_OPT_DP_BANDWISE: one launch per band")
     a = ap.parse_args()
     if a.lib:
         os.environ["DCTE_LIB"] = a.lib
@@ -30,6 +31,8 @@ def main():
     emap = torch.rand((H, W), generator=g, device="cuda", dtype=torch.float32)
     seam = torch.empty(H, dtype=torch.int32, device="cuda")
     with dctenergy.Context(ngpus=1) as ctx:
+        if a.bandwise:
+            ctx.set_option(dctenergy.DCTE_OPT_DP_BANDWISE, 1)
         for _ in range(2):
             ctx.seam_find_tensor(emap, seam)
         torch.cuda.synchronize()
@@ -44,7 +47,7 @@ def main():
         if a.check:
             import oracle_py as O
             ok = bool((seam.cpu().numpy() == O.seam_find(emap.cpu().numpy())).all())
-    print(json.dumps({"tool": "dp_bench", "lib": os.path.basename(a.lib) or "default", "h": H, "w": W,
+    print(json.dumps({"tool": "dp_bench", "lib": os.path.basename(a.lib) or "default", "h": H, "w": W, "bandwise": a.bandwise,
                       "ms_per_seam_search": round(ms, 4), "ns_per_row": round(ms * 1e6 / H, 1),
                       "matches_oracle": ok}), flush=True)
 
