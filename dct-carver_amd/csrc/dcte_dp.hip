@@ -452,17 +452,21 @@ hipError_t launch_seam_find(const DpParams& p, hipStream_t s, bool resident)
     return hipGetLastError();
 }
 
-// tiles the DP can run at once (every tile must be resident: tiles wait on
-// their neighbours)
+// tiles the single-launch DP runs at once: every tile must be resident
+// (tiles wait on their neighbours), and at most one per SIMD.  Two waves per
+// SIMD are resident too, but their polls and steps share one issue port:
+// measured 1.31 us/row at 100000 columns resident vs 0.35 us band-wise
+// (profiles/r02/dp_width.jsonl), so wider frames go band-wise.
 int dp_max_tiles(int device)
 {
+    constexpr int kSimdsPerCu = 4;
     int cus = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
         return 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dcte_seam_dp, kDpLanes, 0) !=
         hipSuccess)
         return 0;
-    return cus * per_cu;
+    return cus * std::min(per_cu, kSimdsPerCu);
 }
 
 }  // namespace dcte
