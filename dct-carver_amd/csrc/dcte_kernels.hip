@@ -590,26 +590,32 @@ __global__ __launch_bounds__(kFixThreads) void dcte_fix(const FixParams p)
     }
 }
 
-// Refinement of a map launch: one wave per 64-column STRIP with flagged
-// pixels (dcte_map keeps a list per strip -- one wave's columns at N <= 8, the
-// whole 64-column tile at N = 16 -- in the row order it emitted them).
-// Tie-dense frames (line art, dots on flat ground) flag a few % of all pixels
-// over most strips; read straight from HBM, one scattered byte per lane,
-// their windows were bound by the texture addresser (17 ms for 7.2 M pixels
-// at 16384^2, profiles/r02).  So each wave works alone (no workgroup
-// barriers; several strips per CU hide each other's latency):
-//  * a strip with few flagged pixels (cnt <= kFixDirect) gathers its windows
-//    from global memory directly, one lane per pixel -- natural frames flag
-//    ~1 pixel per dirty strip;
-//  * a denser strip is walked in bands of SBH output rows: the band's input
-//    rows + window halo are copied to LDS with coalesced dword loads (clamped
-//    per pixel only in strips at the left / right frame border), converted
-//    there ONCE to the reference's fp64 luma, and every window element is one
-//    8-byte LDS read.  Entries come in row-group order, so the wave steps
-//    through them 64 at a time and stages each band once.
-// One lane per pixel for N <= 8 (the window in registers), one 16-lane group
-// per pixel for N = 16 (the window in LDS).
-constexpr unsigned kFixDirect = 32;
+// Refinement of a map launch: one wave per batch of 64-column STRIPs with
+// flagged pixels (dcte_map keeps a list per strip -- one wave's columns at
+// N <= 8, the whole 64-column tile at N = 16 -- in the row order it emitted
+// them).  Tie-dense frames (line art, dots on flat ground) flag a few % of
+// all pixels over most strips; read straight from HBM, one scattered byte per
+// lane, their windows were bound by the texture addresser (17 ms for 7.2 M
+// pixels at 16384^2, profiles/r02).  So each wave works alone (no workgroup
+// barriers; several waves per CU hide each other's latency):
+//  * the sparse strips of a batch (cnt <= kFixDirect<N>) are refined side by
+//    side, one lane group per strip, windows gathered from global memory --
+//    natural frames flag ~1 pixel per dirty strip, text-like frames a few;
+//  * a denser strip is walked by the whole wave in bands of SBH output rows:
+//    the band's input rows + window halo are copied to LDS with coalesced
+//    dword loads (clamped per pixel only in strips at the left / right frame
+//    border), converted there ONCE to the reference's fp64 luma, and every
+//    window element is one 8-byte LDS read.  Entries come in row-group order,
+//    so the wave steps through them 64 at a time and stages each band once;
+//    the next band's list chunk and raw rows load during this band's work.
+// One lane per pixel for N <= 4 (the window in registers), one N-lane group
+// per pixel for N = 8, 16 (the window in LDS).
+// Strips with at most kFixDirect<N> flagged pixels take the direct path: N <= 8
+// at 128 (dots on flat ground, 0.37 % flagged at 16384^2: 0.31 ms vs 0.58 at
+// 32; line art unchanged, worse from 256), N = 16 at 32
+// (profiles/r02/fix_direct.jsonl).
+template <int N>
+constexpr unsigned kFixDirect = N == 16 ? 32u : 128u;
 
 template <int N, int SEM>
 struct FixStrip {
@@ -624,10 +630,10 @@ struct FixStrip {
     static constexpr int LR = SBH + N - 1;            // input rows staged per band
 };
 
-__device__ __forceinline__ int wave_min(int v)
+__device__ __forceinline__ unsigned wave_max_u(unsigned v)
 {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, o));
     return v;
 }
 
@@ -681,7 +687,8 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
     __shared__ double win[kGroup ? PPW : 1][WS];
     const MapParams& p = tp.m;
     const unsigned ndirty = *p.dirty_count;
-    if (blockIdx.x >= ndirty) return;                  // uniform
+    constexpr int SB = kGroup ? PPW : 8;               // strips per batch (below)
+    if (blockIdx.x * SB >= ndirty) return;             // uniform
     const int lane = threadIdx.x;
 #pragma unroll
     for (int t = 0; t < 4; t++) lut[lane + 64 * t] = (double)(lane + 64 * t) / 255;
@@ -716,127 +723,138 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
     };
     auto band_of = [](unsigned loc) { return (((int)(loc >> 6) + N - 1) / G) / FS::GPS; };
 
-    for (unsigned k = blockIdx.x; k < ndirty; k += gridDim.x) {
-        const unsigned strip = p.dirty_list[k];
-        const unsigned cnt = p.tile_count[strip];
+    // strip geometry: first column, output rows [ys, ye), refinement list
+    struct StripGeo {
+        int sx0, ys, ye;
+        const unsigned* list;
+    };
+    auto geo = [&](unsigned strip) {
+        StripGeo g;
         const unsigned tile = strip / SPT;
         const int bx = (int)(tile % (unsigned)tp.tiles_x), by = (int)(tile / (unsigned)tp.tiles_x);
-        const int sx0 = bx * TW + 64 * (int)(strip % SPT);
-        const int ys = p.y0 + by * p.tile_h, ye = min(ys + p.tile_h, p.y1);
-        const unsigned* list = p.fix_list + (size_t)strip * (size_t)(64 * p.tile_h);
-        if (tp.fix_total && lane == 0) atomicAdd(tp.fix_total, cnt);
-        auto store = [&](int lx, int ly, double m, bool edge) {
-            p.out[(long long)(ys + ly - p.y0) * p.out_stride + sx0 + lx] =
-                edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
-        };
+        g.sx0 = bx * TW + 64 * (int)(strip % SPT);
+        g.ys = p.y0 + by * p.tile_h;
+        g.ye = min(g.ys + p.tile_h, p.y1);
+        g.list = p.fix_list + (size_t)strip * (size_t)(64 * p.tile_h);
+        return g;
+    };
+    auto store_at = [&](const StripGeo& g, int lx, int ly, double m, bool edge) {
+        p.out[(long long)(g.ys + ly - p.y0) * p.out_stride + g.sx0 + lx] =
+            edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
+    };
 
-        if (cnt <= kFixDirect) {
-            // sparse strip: windows straight from global memory
-            if constexpr (!kGroup) {
-                if ((unsigned)lane < cnt) {
-                    const unsigned loc = list[lane];
+    // Dirty strips in batches of SB, one group of GL lanes per strip.  The
+    // batch's sparse strips (cnt <= kFixDirect<N>) are refined side by side, their
+    // windows gathered straight from global memory, so their latency chains
+    // (dirty list -> count -> entries -> window bytes) overlap; its dense
+    // strips follow one at a time, each walked by the whole wave.
+    constexpr int GL = 64 / SB;
+    const int sgi = lane / GL, sl = lane % GL;
+    for (unsigned k0 = blockIdx.x * SB; k0 < ndirty; k0 += gridDim.x * SB) {   // uniform
+        const unsigned kk = k0 + sgi;
+        unsigned my_strip = 0, my_cnt = 0;
+        if (kk < ndirty) {
+            my_strip = p.dirty_list[kk];
+            my_cnt = p.tile_count[my_strip];
+        }
+        if (tp.fix_total && sl == 0 && my_cnt) atomicAdd(tp.fix_total, my_cnt);
+        const bool sparse = my_cnt <= kFixDirect<N>;
+        const StripGeo sg = geo(my_strip);
+        const unsigned smax = wave_max_u(sparse ? my_cnt : 0u);
+        if constexpr (!kGroup) {
+            // lane sl of the group: entries sl, sl + GL, ... of its strip
+            for (unsigned i0 = 0; i0 < smax; i0 += GL) {                 // uniform
+                const unsigned i = i0 + sl;
+                if (sparse && i < my_cnt) {
+                    const unsigned loc = sg.list[i];
                     const int ly = (int)(loc >> 6), lx = (int)(loc & 63);
                     double d[N * N];
 #pragma unroll
-                    for (int i = 0; i < N; i++)
+                    for (int ii = 0; ii < N; ii++)
 #pragma unroll
                         for (int j = 0; j < N; j++) {
                             int ox, oy;
-                            offs(i, j, ox, oy);
-                            d[i * N + j] = luma(pixel(clampi(sx0 + lx + ox - HL, 0, p.w - 1),
-                                                      clampi(ys + ly + oy - HL, 0, p.h - 1)));
+                            offs(ii, j, ox, oy);
+                            d[ii * N + j] = luma(pixel(clampi(sg.sx0 + lx + ox - HL, 0, p.w - 1),
+                                                       clampi(sg.ys + ly + oy - HL, 0, p.h - 1)));
                         }
                     double m;
                     bool edge;
                     refine_regs<N>(d, tp.ct, m, edge);
-                    store(lx, ly, m, edge);
-                }
-            } else {
-                // group g: pixel q0 + g; lane l gathers window line l
-                const int l = lane & (N - 1), grp = lane / N;
-                double* d = win[grp];
-                for (unsigned q0 = 0; q0 < cnt; q0 += PPW) {          // uniform
-                    const unsigned q = q0 + grp;
-                    const bool valid = q < cnt;
-                    int lx = 0, ly = 0;
-                    if (valid) {
-                        const unsigned loc = list[q];
-                        ly = (int)(loc >> 6);
-                        lx = (int)(loc & 63);
-#pragma unroll
-                        for (int t = 0; t < N; t++) {
-                            int ox, oy;
-                            offs(t, l, ox, oy);
-                            d[t * (N + 1) + l] = luma(pixel(clampi(sx0 + lx + ox - HL, 0, p.w - 1),
-                                                            clampi(ys + ly + oy - HL, 0, p.h - 1)));
-                        }
-                    }
-                    wave_sync_lds();
-                    // the group transforms its window in place (d[i][j] = d[i * (N + 1) + j])
-                    if constexpr (N == 8) r64::step8(d + l, N + 1); else r64::step16(d + l, N + 1);
-                    wave_sync_lds();
-                    if constexpr (N == 8) r64::step8(d + (N + 1) * l, 1); else r64::step16(d + (N + 1) * l, 1);
-                    wave_sync_lds();
-                    double v[N];
-#pragma unroll
-                    for (int c = 0; c < N; c++) v[c] = d[l * (N + 1) + c];
-                    double best;
-                    bool edge;
-                    lastmax_group<N>(v, l, best, edge);
-                    if (valid && l == 0) store(lx, ly, best, edge);
-                    wave_sync_lds();
+                    store_at(sg, lx, ly, m, edge);
                 }
             }
-            continue;
+        } else {
+            // the group (GL = N lanes) takes its strip's entries one at a
+            // time; lane l gathers window line l
+            const int l = sl;
+            double* d = win[sgi];
+            for (unsigned i = 0; i < smax; i++) {                         // uniform
+                const bool valid = sparse && i < my_cnt;
+                int lx = 0, ly = 0;
+                if (valid) {
+                    const unsigned loc = sg.list[i];
+                    ly = (int)(loc >> 6);
+                    lx = (int)(loc & 63);
+#pragma unroll
+                    for (int t = 0; t < N; t++) {
+                        int ox, oy;
+                        offs(t, l, ox, oy);
+                        d[t * (N + 1) + l] = luma(pixel(clampi(sg.sx0 + lx + ox - HL, 0, p.w - 1),
+                                                        clampi(sg.ys + ly + oy - HL, 0, p.h - 1)));
+                    }
+                }
+                wave_sync_lds();
+                // the group transforms its window in place (d[i][j] = d[i * (N + 1) + j])
+                if constexpr (N == 8) r64::step8(d + l, N + 1); else r64::step16(d + l, N + 1);
+                wave_sync_lds();
+                if constexpr (N == 8) r64::step8(d + (N + 1) * l, 1); else r64::step16(d + (N + 1) * l, 1);
+                wave_sync_lds();
+                double v[N];
+#pragma unroll
+                for (int c = 0; c < N; c++) v[c] = d[l * (N + 1) + c];
+                double best;
+                bool edge;
+                lastmax_group<N>(v, l, best, edge);
+                if (valid && l == 0) store_at(sg, lx, ly, best, edge);
+                wave_sync_lds();
+            }
         }
 
-        // dense strip, band by band.  The entries are sorted by band (the map
-        // kernel emits them group by group; band = group / GPS), so a band's
-        // entries are a contiguous run [pos, end) of the list.
-        const bool interior = sx0 - HL >= 0 && (sx0 - HL + LW) * BPP + 3 <= p.w * BPP;
-        for (unsigned pos = 0; pos < cnt;) {                           // uniform
-            // the run's end and the luma columns its windows need (a 128-bit
-            // mask); a run of <= 64 entries stays in registers (loc0)
-            unsigned end = pos, loc0 = 0;
-            int b = 0;
-            bool single = true;
-            uint64_t mlo = 0, mhi = 0;
-            for (int chunk = 0;; chunk++) {
-                const unsigned q = end + lane;
-                const unsigned loc = q < cnt ? list[q] : 0u;
-                if (chunk == 0) {
-                    b = band_of(__shfl(loc, 0));
-                    loc0 = loc;
-                }
-                const bool in = q < cnt && band_of(loc) == b;
-                if (in) {
-                    constexpr uint64_t bits = (1ull << N) - 1;
-                    const int lx = (int)(loc & 63);
-                    mlo |= bits << lx;
-                    if (lx + N > 64) mhi |= bits >> (64 - lx);
-                }
-                const int nin = __popcll(__ballot(in));     // a prefix of the lanes
-                end += nin;
-                if (nin < 64) break;
-                single = false;
-            }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                mlo |= __shfl_xor(mlo, o);
-                mhi |= __shfl_xor(mhi, o);
-            }
-            const uint32_t m0 = (uint32_t)mlo, m1 = (uint32_t)(mlo >> 32), m2 = (uint32_t)mhi;
-            // band b: output rows [max(A, 0), min(A + SBH, ye - ys)), A = b SBH - (N - 1);
-            // input rows from r0 = max(A, 0) - HL (tile-relative)
-            const int A = b * SBH - (N - 1);
-            const int r0 = max(A, 0) - HL;
-            const int nrows = min(A + SBH, ye - ys) - max(A, 0) + N - 1;
-            // raw bytes of the band's rows
-            if (interior) {
-                constexpr int SPAN = LW * BPP;
-                constexpr int U = (LR * PDW + 63) / 64;
-                uint32_t v[U];
-#pragma unroll
+        // the batch's dense strips, one at a time
+        uint64_t dense_mask = __ballot(!sparse && sl == 0);
+        while (dense_mask) {                                              // uniform
+            const int leader = __builtin_ctzll(dense_mask);             // lane 0 of its group
+            dense_mask &= dense_mask - 1;
+            const unsigned strip = __shfl(my_strip, leader);
+            const unsigned cnt = __shfl(my_cnt, leader);
+            const StripGeo dg = geo(strip);
+            const int sx0 = dg.sx0, ys = dg.ys, ye = dg.ye;
+            const unsigned* list = dg.list;
+            auto store = [&](int lx, int ly, double m, bool edge) { store_at(dg, lx, ly, m, edge); };
+
+            // dense strip, band by band.  The entries are sorted by band (the map
+            // kernel emits them group by group; band = group / GPS), so a band's
+            // entries are a contiguous run [pos, end) of the list.  Software
+            // pipelined: the next run's first list chunk and (interior strips) its
+            // band's raw rows are in flight while this band converts and computes.
+            const bool interior = sx0 - HL >= 0 && (sx0 - HL + LW) * BPP + 3 <= p.w * BPP;
+            constexpr int SPAN = LW * BPP;
+            constexpr int U = (LR * PDW + 63) / 64;
+            auto band_rows = [&](int bb, int& r0, int& nrows) {
+                // band bb: output rows [max(A, 0), min(A + SBH, ye - ys)), A = bb SBH - (N - 1);
+                // input rows from r0 = max(A, 0) - HL (tile-relative)
+                const int A = bb * SBH - (N - 1);
+                r0 = max(A, 0) - HL;
+                nrows = min(A + SBH, ye - ys) - max(A, 0) + N - 1;
+            };
+            uint32_t v[U];
+            // raw dwords of band bb -> v (interior strips: every row's span is in
+            // the frame); each row's misalignment -> mis
+            auto issue_raw = [&](int bb) {
+                int r0, nrows;
+                band_rows(bb, r0, nrows);
+    #pragma unroll
                 for (int u = 0; u < U; u++) {
                     const int e = lane + 64 * u;
                     const int r = e / PDW, dw = e - r * PDW;
@@ -850,79 +868,151 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
                             v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)((a & ~3u) + 4u * dw), 0, 0);
                     }
                 }
-#pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const int e = lane + 64 * u;
-                    if (e < nrows * PDW) raw[e] = v[u];
+            };
+            unsigned loc = (unsigned)lane < cnt ? list[lane] : 0u;      // the first run's first chunk
+            int b = band_of(__shfl(loc, 0));
+            if (interior) issue_raw(b);
+            for (unsigned pos = 0; pos < cnt;) {                           // uniform
+                // the run's end and the luma columns its windows need (a 128-bit
+                // mask); a run of <= 64 entries stays in registers (loc0)
+                unsigned end = pos;
+                const unsigned loc0 = loc;
+                bool single = true;
+                uint64_t mlo = 0, mhi = 0;
+                for (int chunk = 0;; chunk++) {
+                    const unsigned q = end + lane;
+                    const unsigned lc = chunk == 0 ? loc : (q < cnt ? list[q] : 0u);
+                    const bool in = q < cnt && band_of(lc) == b;
+                    if (in) {
+                        constexpr uint64_t bits = (1ull << N) - 1;
+                        const int lx = (int)(lc & 63);
+                        mlo |= bits << lx;
+                        if (lx + N > 64) mhi |= bits >> (64 - lx);
+                    }
+                    const int nin = __popcll(__ballot(in));     // a prefix of the lanes
+                    end += nin;
+                    if (nin < 64) break;
+                    single = false;
                 }
-            } else {
-                for (int e = lane; e < nrows * LW; e += 64) {
-                    const int r = e / LW, c = e - r * LW;
-                    const uint8_t* src = pixel(clampi(sx0 - HL + c, 0, p.w - 1), clampi(ys + r0 + r, 0, p.h - 1));
-                    uint8_t* dst = reinterpret_cast<uint8_t*>(&raw[r * PDW]) + c * BPP;
-#pragma unroll
-                    for (int ch = 0; ch < BPP; ch++) dst[ch] = src[ch];
-                    if (c == 0) mis[r] = 0;
+                // the next run's first chunk, in flight through this band
+                const unsigned locN = end + lane < cnt ? list[end + lane] : 0u;
+    #pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    mlo |= __shfl_xor(mlo, o);
+                    mhi |= __shfl_xor(mhi, o);
                 }
+                const uint32_t m0 = (uint32_t)mlo, m1 = (uint32_t)(mlo >> 32), m2 = (uint32_t)mhi;
+                int r0, nrows;
+                band_rows(b, r0, nrows);
+                // raw bytes of the band's rows
+                if (interior) {
+    #pragma unroll
+                    for (int u = 0; u < U; u++) {
+                        const int e = lane + 64 * u;
+                        if (e < nrows * PDW) raw[e] = v[u];
+                    }
+                } else {
+                    for (int e = lane; e < nrows * LW; e += 64) {
+                        const int r = e / LW, c = e - r * LW;
+                        const uint8_t* src = pixel(clampi(sx0 - HL + c, 0, p.w - 1), clampi(ys + r0 + r, 0, p.h - 1));
+                        uint8_t* dst = reinterpret_cast<uint8_t*>(&raw[r * PDW]) + c * BPP;
+    #pragma unroll
+                        for (int ch = 0; ch < BPP; ch++) dst[ch] = src[ch];
+                        if (c == 0) mis[r] = 0;
+                    }
+                }
+                // the needed columns, compacted
+                const int n0 = __popc(m0), n1 = __popc(m1);
+                const int ncols = n0 + n1 + __popc(m2);
+                for (int c = lane; c < LW; c += 64) {
+                    const uint32_t word = c < 32 ? m0 : (c < 64 ? m1 : m2);
+                    const int bit = c & 31;
+                    if ((word >> bit) & 1u) {
+                        const int before = (c < 32 ? 0 : (c < 64 ? n0 : n0 + n1)) +
+                                           __popc(word & ((1u << bit) - 1u));
+                        colidx[before] = (unsigned char)c;
+                    }
+                }
+                wave_sync_lds();
+                // fp64 luma of the needed columns, kConv elements per lane at a time
+                // (their LDS round trips overlap)
+                constexpr int kConv = 4;
+                const float inv = 1.0f / (float)max(ncols, 1);
+                const int total = nrows * ncols;
+    #ifdef DCTE_FIX_SKIP_CONV   // timing probe only: wrong results
+                for (int e0 = lane; e0 < 0; e0 += 64 * kConv) {
+    #else
+                for (int e0 = lane; e0 < total; e0 += 64 * kConv) {
+    #endif
+                    int at[kConv], cc[kConv];
+    #pragma unroll
+                    for (int k = 0; k < kConv; k++) {
+                        const int e = min(e0 + 64 * k, total - 1);  // tail: repeat the last element
+                        int r = (int)((float)e * inv);             // e / ncols, corrected (e < 2^12)
+                        r += (r + 1) * ncols <= e;
+                        r -= r * ncols > e;
+                        at[k] = r;
+                        cc[k] = e - r * ncols;
+                    }
+    #pragma unroll
+                    for (int k = 0; k < kConv; k++) cc[k] = colidx[cc[k]];
+                    double lv[kConv];
+    #pragma unroll
+                    for (int k = 0; k < kConv; k++)
+                        lv[k] = luma(reinterpret_cast<const uint8_t*>(&raw[at[k] * PDW]) + mis[at[k]] + cc[k] * BPP);
+    #pragma unroll
+                    for (int k = 0; k < kConv; k++) lum[at[k] * LW + cc[k]] = lv[k];
+                }
+                wave_sync_lds();
+                // the next run's band: its raw rows in flight through this band's compute
+                int bN = b;
+                if (end < cnt) {                                       // uniform
+                    bN = band_of(__shfl(locN, 0));
+                    if (interior) issue_raw(bN);
+                }
+                // element (i, j) of pixel (lx, ly): lum row ly + oy - HL - r0, column lx + ox
+                if constexpr (!kGroup) {
+                    for (unsigned q = pos + lane; q < end; q += 64) {
+                        const unsigned lc = single ? loc0 : list[q];
+                        const int ly = (int)(lc >> 6), lx = (int)(lc & 63);
+                        const double* base = &lum[(ly - HL - r0) * LW + lx];
+                        double d[N * N];
+    #pragma unroll
+                        for (int i = 0; i < N; i++)
+    #pragma unroll
+                            for (int j = 0; j < N; j++) {
+                                int ox, oy;
+                                offs(i, j, ox, oy);
+                                d[i * N + j] = base[oy * LW + ox];
+                            }
+                        double m;
+                        bool edge;
+                        refine_regs<N>(d, tp.ct, m, edge);
+                        store(lx, ly, m, edge);
+                    }
+                } else {
+                    const int l = lane & (N - 1), grp = lane / N;
+    #ifdef DCTE_FIX_SKIP_COMPUTE   // timing probe only: wrong results
+                    for (unsigned q0 = pos; q0 < pos; q0 += PPW) {
+    #else
+                    for (unsigned q0 = pos; q0 < end; q0 += PPW) {        // uniform
+    #endif
+                        const unsigned q = q0 + grp;
+                        const bool valid = q < end;
+                        const unsigned lq = __shfl(loc0, (int)(q - pos) & 63);
+                        const unsigned lc = single ? (valid ? lq : loc0) : list[valid ? q : pos];
+                        const int ly = (int)(lc >> 6), lx = (int)(lc & 63);
+                        double best;
+                        bool edge;
+                        refine_group<N, SEM>(lum, LW, (ly - HL - r0) * LW + lx, win[grp], l, best, edge);
+                        if (valid && l == 0) store(lx, ly, best, edge);
+                    }
+                }
+                wave_sync_lds();                           // lum / raw / colidx free for the next band
+                pos = end;
+                loc = locN;
+                b = bN;
             }
-            // the needed columns, compacted
-            const int n0 = __popc(m0), n1 = __popc(m1);
-            const int ncols = n0 + n1 + __popc(m2);
-            for (int c = lane; c < LW; c += 64) {
-                const uint32_t word = c < 32 ? m0 : (c < 64 ? m1 : m2);
-                const int bit = c & 31;
-                if ((word >> bit) & 1u) {
-                    const int before = (c < 32 ? 0 : (c < 64 ? n0 : n0 + n1)) +
-                                       __popc(word & ((1u << bit) - 1u));
-                    colidx[before] = (unsigned char)c;
-                }
-            }
-            wave_sync_lds();
-            const float inv = 1.0f / (float)max(ncols, 1);
-            for (int e = lane; e < nrows * ncols; e += 64) {
-                int r = (int)((float)e * inv);                 // e / ncols, corrected (e < 2^12)
-                r += (r + 1) * ncols <= e;
-                r -= r * ncols > e;
-                const int c = colidx[e - r * ncols];
-                lum[r * LW + c] = luma(reinterpret_cast<const uint8_t*>(&raw[r * PDW]) + mis[r] + c * BPP);
-            }
-            wave_sync_lds();
-            // element (i, j) of pixel (lx, ly): lum row ly + oy - HL - r0, column lx + ox
-            if constexpr (!kGroup) {
-                for (unsigned q = pos + lane; q < end; q += 64) {
-                    const unsigned loc = single ? loc0 : list[q];
-                    const int ly = (int)(loc >> 6), lx = (int)(loc & 63);
-                    const double* base = &lum[(ly - HL - r0) * LW + lx];
-                    double d[N * N];
-#pragma unroll
-                    for (int i = 0; i < N; i++)
-#pragma unroll
-                        for (int j = 0; j < N; j++) {
-                            int ox, oy;
-                            offs(i, j, ox, oy);
-                            d[i * N + j] = base[oy * LW + ox];
-                        }
-                    double m;
-                    bool edge;
-                    refine_regs<N>(d, tp.ct, m, edge);
-                    store(lx, ly, m, edge);
-                }
-            } else {
-                const int l = lane & (N - 1), grp = lane / N;
-                for (unsigned q0 = pos; q0 < end; q0 += PPW) {        // uniform
-                    const unsigned q = q0 + grp;
-                    const bool valid = q < end;
-                    const unsigned lq = __shfl(loc0, (int)(q - pos) & 63);
-                    const unsigned loc = single ? (valid ? lq : loc0) : list[valid ? q : pos];
-                    const int ly = (int)(loc >> 6), lx = (int)(loc & 63);
-                    double best;
-                    bool edge;
-                    refine_group<N, SEM>(lum, LW, (ly - HL - r0) * LW + lx, win[grp], l, best, edge);
-                    if (valid && l == 0) store(lx, ly, best, edge);
-                }
-            }
-            wave_sync_lds();                           // lum / raw / colidx free for the next band
-            pos = end;
         }
     }
 }

@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--n", type=int, default=8)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--lib", default=None)
+    ap.add_argument("--tau", type=float, default=4e-6)
     a = ap.parse_args()
     if a.lib:
         os.environ["DCTE_LIB"] = os.path.abspath(a.lib)
@@ -28,6 +29,7 @@ def main():
     fr = {k.split()[0]: v for k, v in fix_study.frames(a.size, torch, dev).items()}[a.frame]
     out = torch.empty((a.size, a.size), dtype=torch.float32, device=dev)
     with dctenergy.Context(ngpus=1) as ctx:
+        ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, a.tau)
         for _ in range(a.iters):
             ctx.energy_map_tensor(fr, out, a.n, 0.3, 0.7)
         torch.cuda.synchronize()

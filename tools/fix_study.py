@@ -3,9 +3,11 @@
     python tools/fix_study.py [--size 16384] [--n 8] [--iters 10]
 
 For each frame kind: the number of pixels the map kernel flags (e != t, so
-the class matters), and the device time of the map launch alone (refinement
-off, tie_tau = 0) vs map + refinement (default tau), HIP events on the launch
-stream.  One JSON line per frame.  Line art and isolated dots on flat ground
+the class matters), the device time of the map launch (HIP events around
+it, DCTE_OPT_PROFILE) and of the whole call, map + refinement (HIP events on
+the stream); fix_ms is their difference.  refinement_off_ms: the call with
+tau = 0 (no refinement launch), for reference.  One JSON line per frame.
+Line art and isolated dots on flat ground
 hold exact edge/texture ties in real arithmetic (decided only by the
 reference's rounding, src/dct.c:100-108), so they are the worst realistic
 inputs for the refinement.
@@ -52,6 +54,7 @@ def main():
     ap.add_argument("--edges", type=float, default=0.3)
     ap.add_argument("--textures", type=float, default=0.7)
     ap.add_argument("--lib", default=None, help="libdctenergy_hip.so to load (A/B)")
+    ap.add_argument("--frames", default="", help="comma-separated frame-name prefixes (default: all)")
     a = ap.parse_args()
     if a.lib:
         os.environ["DCTE_LIB"] = os.path.abspath(a.lib)
@@ -62,24 +65,38 @@ def main():
     out = torch.empty((S, S), dtype=torch.float32, device=dev)
     with dctenergy.Context(ngpus=1) as ctx:
         for name, fr in frames(S, torch, dev).items():
+            if a.frames and not any(name.startswith(f) for f in a.frames.split(",")):
+                continue
             stream = torch.cuda.current_stream(dev)
 
             def timed(tau):
+                """-> (stream ms per call, map-launch ms per call)"""
                 ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, tau)
                 ctx.energy_map_tensor(fr, out, n, e, t)        # warm
+                torch.cuda.synchronize()
+                ctx.profile_read()
+                ctx.set_option(dctenergy.DCTE_OPT_PROFILE, 1)
                 a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a0.record(stream)
                 for _ in range(a.iters):
                     ctx.energy_map_tensor(fr, out, n, e, t)
                 a1.record(stream)
                 torch.cuda.synchronize()
-                return a0.elapsed_time(a1) / a.iters
+                ctx.set_option(dctenergy.DCTE_OPT_PROFILE, 0)
+                _, kms = ctx.profile_read()
+                return a0.elapsed_time(a1) / a.iters, kms / a.iters
 
-            # interleaved rounds, best of each (clock ramps and neighbours on the box)
-            ms_map, ms_all = 1e9, 1e9
+            # interleaved rounds, best of each (clock ramps and neighbours on the box).
+            # The refinement's cost is the call minus its own map launch (HIP
+            # events around that launch), not minus a separate tau = 0 run:
+            # on some boxes those ran 0.1-0.2 ms slower per call than the
+            # default calls, on others not.
+            ms_off, ms_all, ms_kern = 1e9, 1e9, 1e9
             for _ in range(3):
-                ms_map = min(ms_map, timed(0.0))
-                ms_all = min(ms_all, timed(4e-6))
+                ms_off = min(ms_off, timed(0.0)[0])
+                tot, kern = timed(4e-6)
+                ms_all, ms_kern = min(ms_all, tot), min(ms_kern, kern)
+            ms_map = ms_kern
             ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, 4e-6)
             # flagged count: the host entry point reports it (same kernels)
             host = fr.cpu().numpy()
@@ -90,6 +107,7 @@ def main():
                    "flagged": flagged,
                    "flagged_frac": round(flagged / (S * S), 5),
                    "map_ms": round(ms_map, 4), "map_plus_fix_ms": round(ms_all, 4),
+                   "refinement_off_ms": round(ms_off, 4),
                    "fix_ms": round(ms_all - ms_map, 4),
                    "fix_frac_of_map": round((ms_all - ms_map) / ms_map, 4)}
             print(json.dumps(res), flush=True)
