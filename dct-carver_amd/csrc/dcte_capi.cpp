@@ -108,6 +108,7 @@ struct dcte_ctx {
     double pin_mib = 64.0;          // DCTE_OPT_PIN_HOST
     int tile_h = 0;                 // DCTE_OPT_TILE_H (0: the kernel's default)
     bool dp_bandwise = false;       // DCTE_OPT_DP_BANDWISE
+    unsigned dp_spin_limit = 0;     // DCTE_OPT_DP_SPIN_LIMIT (0: the kernel's default)
     std::vector<ProfEvent> prof;
     long long last_refined = 0;
     std::string last_error;
@@ -611,6 +612,14 @@ int dcte_set_option(dcte_ctx* ctx, int option, double value)
     case DCTE_OPT_DP_BANDWISE:
         ctx->dp_bandwise = value != 0;
         return DCTE_OK;
+    case DCTE_OPT_DP_SPIN_LIMIT:
+        if (!(value >= 0 && value <= 4294967295.0)) return DCTE_EINVAL;
+        ctx->dp_spin_limit = (unsigned)value;
+        // re-enables the single-launch search on streams a timeout moved to
+        // band-wise launches
+        for (Device& d : ctx->devs)
+            for (auto& kv : d.dp) kv.second.max_tiles = -1;
+        return DCTE_OK;
     default: return DCTE_EINVAL;
     }
 }
@@ -893,6 +902,7 @@ int dcte_seam_find_device(dcte_ctx* ctx, int device, const float* d_map, long lo
     p.bx = p.sx + p.ns;
     p.err = reinterpret_cast<unsigned*>(p.bx + p.nb);
     p.seam = d_seam;
+    p.spin_limit = ctx->dp_spin_limit;
     DCTE_HIP(ctx, hipMemsetAsync(p.err, 0, sizeof(unsigned), s));
     DCTE_HIP(ctx, dcte::launch_seam_find(p, s, resident));
     return DCTE_OK;

@@ -182,6 +182,7 @@ void dcte_seam_dp(const DpParams p)
         bool need[C];
 #pragma unroll
         for (int c = 0; c < C; c++) need[c] = in[c] && !own;
+        const unsigned limit = p.spin_limit ? p.spin_limit : kDpSpinLimit;
         unsigned spins = 0;
         for (;;) {
             unsigned long long v[C];
@@ -198,13 +199,13 @@ void dcte_seam_dp(const DpParams p)
                     if (need[c]) m[c] = __int_as_float((int)(unsigned)v[c]);
                 return true;
             }
-            if ((++spins & 255) == 0) {
-                if (spins > kDpSpinLimit) {
-                    __hip_atomic_fetch_or(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    return false;
-                }
-                if (__hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+            if (++spins >= limit) {
+                __hip_atomic_fetch_or(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return false;
             }
+            if ((spins & 255) == 0 &&
+                __hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                return false;
             __builtin_amdgcn_s_sleep(1);
         }
     };

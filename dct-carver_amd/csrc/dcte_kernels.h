@@ -109,6 +109,7 @@ struct DpParams {
     int* bx;                 // nb
     unsigned* err;           // 1, zeroed before the launch
     int* seam;               // h: column removed per row (-1 everywhere on failure)
+    unsigned spin_limit;     // polls before a waiting tile gives up (0: the default)
     int j0, j1;              // dcte_seam_dp: bands [j0, j1) in this launch; j0 > 0 starts
                              // from band j0 - 1's published row (launched one band at a
                              // time when not every tile can be resident)

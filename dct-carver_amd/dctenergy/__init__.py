@@ -34,6 +34,7 @@ DCTE_OPT_PROFILE = 2
 DCTE_OPT_PIN_HOST = 3
 DCTE_OPT_TILE_H = 4
 DCTE_OPT_DP_BANDWISE = 5
+DCTE_OPT_DP_SPIN_LIMIT = 6
 DCTE_NORM_LQR = 0
 DCTE_NORM_PREVIEW = 1
 DCTE_CREATE_SAME_DEVICE = 1
@@ -425,5 +426,5 @@ class Context:
 
 
 __all__ = ["Context", "DcteError", "lib", "device_count", "LIB_PATH", "EXPORTS",
-           "DCTE_LQR", "DCTE_PREVIEW", "DCTE_OPT_TIE_TAU", "DCTE_OPT_PROFILE", "DCTE_OPT_PIN_HOST", "DCTE_OPT_TILE_H", "DCTE_OPT_DP_BANDWISE",
+           "DCTE_LQR", "DCTE_PREVIEW", "DCTE_OPT_TIE_TAU", "DCTE_OPT_PROFILE", "DCTE_OPT_PIN_HOST", "DCTE_OPT_TILE_H", "DCTE_OPT_DP_BANDWISE", "DCTE_OPT_DP_SPIN_LIMIT",
            "DCTE_NORM_LQR", "DCTE_NORM_PREVIEW"]

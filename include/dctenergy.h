@@ -83,6 +83,15 @@ extern "C" {
                                rows even when every DP tile fits on the chip
                                (the mode frames wider than that use; no tile
                                then waits on another); same seams */
+#define DCTE_OPT_DP_SPIN_LIMIT 6 /* polls after which a tile of the single-launch
+                               seam search stops waiting for a neighbour (0 =
+                               default, ~0.5 s; small values are for testing
+                               the time-out path).  A timed-out search returns
+                               seam = -1 from the device entry point; the host
+                               entry points (dcte_seam_find, dcte_carve) run it
+                               again band-wise and keep that stream band-wise.
+                               Setting this option re-enables the single
+                               launch. */
 
 typedef struct dcte_ctx dcte_ctx;
 

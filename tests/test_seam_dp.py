@@ -89,6 +89,43 @@ def test_carve_bandwise_equals_resident(ctx):
     assert np.array_equal(out, ref) and np.array_equal(cols, ref_cols)
 
 
+def test_seam_timeout_falls_back_to_bandwise(ctx):
+    """DCTE_OPT_DP_SPIN_LIMIT = 1: a tile of the single-launch search gives up
+    the first time a neighbour's row is not there yet.  The device entry point
+    reports that as seam = -1; the host entry points run the search again one
+    launch per band and return the oracle's seam."""
+    import torch
+    h, w = 16384, 4096               # 512 hand-offs per tile: some must wait
+    E = _maps(h, w, "valley", 11)
+    ref = O.seam_find(E)
+    d_map = torch.from_numpy(E).cuda()
+    seam = torch.empty(h, dtype=torch.int32, device="cuda")
+    ctx.set_option(dctenergy.DCTE_OPT_DP_SPIN_LIMIT, 1)
+    try:
+        ctx.seam_find_tensor(d_map, seam)
+        torch.cuda.synchronize()
+        dev = seam.cpu().numpy()
+        host = ctx.seam_find(E)              # times out, then runs band-wise
+        again = ctx.seam_find(E)             # this stream stays band-wise
+    finally:
+        ctx.set_option(dctenergy.DCTE_OPT_DP_SPIN_LIMIT, 0)
+    assert (dev == -1).all()
+    assert np.array_equal(host, ref) and np.array_equal(again, ref)
+    assert np.array_equal(ctx.seam_find(E), ref)   # single launch again
+
+
+def test_carve_timeout_falls_back_to_bandwise(ctx):
+    """dcte_carve whose searches time out runs the whole carve again band-wise."""
+    img = np.random.default_rng(5).integers(0, 256, (8192, 320, 3), dtype=np.uint8)
+    ref, ref_cols = ctx.carve(img, 3, 8, 0.5, 0.5)
+    ctx.set_option(dctenergy.DCTE_OPT_DP_SPIN_LIMIT, 1)
+    try:
+        out, cols = ctx.carve(img, 3, 8, 0.5, 0.5)
+    finally:
+        ctx.set_option(dctenergy.DCTE_OPT_DP_SPIN_LIMIT, 0)
+    assert np.array_equal(out, ref) and np.array_equal(cols, ref_cols)
+
+
 def test_seam_bad_arguments(ctx):
     L = dctenergy.lib()
     seam = np.empty(4, np.int32)
