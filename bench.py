@@ -140,6 +140,14 @@ def cpu_baseline(frame_rows_host, W, n, e, t, sample_rows):
                          f"(oracle/_ref) per pixel in liblqr build order, luma precomputed, "
                          f"OpenMP over rows on {threads} threads, {dt:.2f} s wall = "
                          f"{dt * threads:.1f} thread-s"}
+        # the reference as it runs in the plug-in: one thread (liblqr calls
+        # the callback serially, src/render.c:314-315)
+        rows1 = min(64, sample_rows)
+        t0 = time.perf_counter()
+        O.ref_energy_map_luma_rows(L, n, e, t, y0=0, y1=rows1, h=L.shape[0], nthreads=1)
+        d1 = time.perf_counter() - t0
+        res["single_thread"] = {"value": round(rows1 * W / d1 / 1e6, 3), "unit": "Mpx/s",
+                                "cores": 1, "sample": f"output rows 0..{rows1 - 1}, {d1:.2f} s"}
     t0 = time.perf_counter()
     O.energy_map(img, n, e, t, y0=0, y1=sample_rows, nthreads=threads)
     dp = time.perf_counter() - t0
