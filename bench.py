@@ -439,7 +439,8 @@ def main():
                 "px_per_rank": px_per_rank,
                 "launches_timed": launches,
                 "note": "rank 0's map launches; binding roof is VALU (see valu) -- the HBM "
-                        "fraction ceiling of this computation is ~24 % (DESIGN.md §4)",
+                        "fraction this computation can reach is bounded by its VALU op count "
+                        "(N=8: ~24 %; DESIGN.md §4)",
             },
             "valu": {
                 "lane_ops_per_px": valu_per_px,
