@@ -854,7 +854,7 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
             auto issue_raw = [&](int bb) {
                 int r0, nrows;
                 band_rows(bb, r0, nrows);
-    #pragma unroll
+#pragma unroll
                 for (int u = 0; u < U; u++) {
                     const int e = lane + 64 * u;
                     const int r = e / PDW, dw = e - r * PDW;
@@ -896,7 +896,7 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
                 }
                 // the next run's first chunk, in flight through this band
                 const unsigned locN = end + lane < cnt ? list[end + lane] : 0u;
-    #pragma unroll
+#pragma unroll
                 for (int o = 32; o > 0; o >>= 1) {
                     mlo |= __shfl_xor(mlo, o);
                     mhi |= __shfl_xor(mhi, o);
@@ -906,7 +906,7 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
                 band_rows(b, r0, nrows);
                 // raw bytes of the band's rows
                 if (interior) {
-    #pragma unroll
+#pragma unroll
                     for (int u = 0; u < U; u++) {
                         const int e = lane + 64 * u;
                         if (e < nrows * PDW) raw[e] = v[u];
@@ -916,7 +916,7 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
                         const int r = e / LW, c = e - r * LW;
                         const uint8_t* src = pixel(clampi(sx0 - HL + c, 0, p.w - 1), clampi(ys + r0 + r, 0, p.h - 1));
                         uint8_t* dst = reinterpret_cast<uint8_t*>(&raw[r * PDW]) + c * BPP;
-    #pragma unroll
+#pragma unroll
                         for (int ch = 0; ch < BPP; ch++) dst[ch] = src[ch];
                         if (c == 0) mis[r] = 0;
                     }
@@ -939,13 +939,9 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
                 constexpr int kConv = 4;
                 const float inv = 1.0f / (float)max(ncols, 1);
                 const int total = nrows * ncols;
-    #ifdef DCTE_FIX_SKIP_CONV   // timing probe only: wrong results
-                for (int e0 = lane; e0 < 0; e0 += 64 * kConv) {
-    #else
                 for (int e0 = lane; e0 < total; e0 += 64 * kConv) {
-    #endif
                     int at[kConv], cc[kConv];
-    #pragma unroll
+#pragma unroll
                     for (int k = 0; k < kConv; k++) {
                         const int e = min(e0 + 64 * k, total - 1);  // tail: repeat the last element
                         int r = (int)((float)e * inv);             // e / ncols, corrected (e < 2^12)
@@ -954,13 +950,13 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
                         at[k] = r;
                         cc[k] = e - r * ncols;
                     }
-    #pragma unroll
+#pragma unroll
                     for (int k = 0; k < kConv; k++) cc[k] = colidx[cc[k]];
                     double lv[kConv];
-    #pragma unroll
+#pragma unroll
                     for (int k = 0; k < kConv; k++)
                         lv[k] = luma(reinterpret_cast<const uint8_t*>(&raw[at[k] * PDW]) + mis[at[k]] + cc[k] * BPP);
-    #pragma unroll
+#pragma unroll
                     for (int k = 0; k < kConv; k++) lum[at[k] * LW + cc[k]] = lv[k];
                 }
                 wave_sync_lds();
@@ -977,9 +973,9 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
                         const int ly = (int)(lc >> 6), lx = (int)(lc & 63);
                         const double* base = &lum[(ly - HL - r0) * LW + lx];
                         double d[N * N];
-    #pragma unroll
+#pragma unroll
                         for (int i = 0; i < N; i++)
-    #pragma unroll
+#pragma unroll
                             for (int j = 0; j < N; j++) {
                                 int ox, oy;
                                 offs(i, j, ox, oy);
@@ -992,11 +988,7 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
                     }
                 } else {
                     const int l = lane & (N - 1), grp = lane / N;
-    #ifdef DCTE_FIX_SKIP_COMPUTE   // timing probe only: wrong results
-                    for (unsigned q0 = pos; q0 < pos; q0 += PPW) {
-    #else
                     for (unsigned q0 = pos; q0 < end; q0 += PPW) {        // uniform
-    #endif
                         const unsigned q = q0 + grp;
                         const bool valid = q < end;
                         const unsigned lq = __shfl(loc0, (int)(q - pos) & 63);
