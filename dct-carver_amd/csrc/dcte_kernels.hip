@@ -678,13 +678,18 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
     constexpr int PPW = kGroup ? 64 / N : 64;          // pixels per wave pass
     __shared__ double lut[256];
     __shared__ double lum[LR * LW];                    // fp64 luma of one band (+ halo), needed columns
-    __shared__ __attribute__((aligned(16))) uint32_t raw[LR * PDW];
     __shared__ unsigned char mis[LR];                  // byte offset of each raw row's first pixel
     __shared__ unsigned char colidx[LW];               // the needed luma columns, ascending
     // per group: N rows of N + 1 doubles, plus a pad that starts consecutive
     // groups 16 banks apart
     constexpr int WS = kGroup ? (N * (N + 1) + 7) / 8 * 8 + 8 : 1;
-    __shared__ double win[kGroup ? PPW : 1][WS];
+    // the band's raw rows and the groups' window buffers share one region:
+    // raw is read only by the luma conversion, the windows only after it
+    // (fewer LDS bytes per wave, more waves per CU)
+    constexpr int RAW_D = (LR * PDW + 1) / 2, WIN_D = (kGroup ? PPW : 1) * WS;
+    __shared__ __attribute__((aligned(16))) double rw_lds[RAW_D > WIN_D ? RAW_D : WIN_D];
+    uint32_t* const raw = reinterpret_cast<uint32_t*>(rw_lds);
+    double (*const win)[WS] = reinterpret_cast<double (*)[WS]>(rw_lds);
     const MapParams& p = tp.m;
     const unsigned ndirty = *p.dirty_count;
     constexpr int SB = kGroup ? PPW : 8;               // strips per batch (below)
@@ -1119,7 +1124,20 @@ static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
     if (p.m.tile_h < 1 || p.tiles_x != (p.m.w + Geo<N, SEM>::TW - 1) / Geo<N, SEM>::TW)
         return hipErrorInvalidValue;
     const int nstrips = p.tiles_x * FixStrip<N, SEM>::SPT * ((p.m.y1 - p.m.y0 + p.m.tile_h - 1) / p.m.tile_h);
-    const int blocks = nstrips < 2048 ? nstrips : 2048;   // one wave each; ~8 per CU
+    // one wave per block, as many as the device holds at once (LDS-bound:
+    // ~10 per CU at N = 8 RGB); each walks the dirty list in strip batches
+    static int resident = 0;
+    if (!resident) {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dcte_fix_strips<N, BPP, SEM>, 64, 0) ==
+                hipSuccess && cus > 0 && per_cu > 0)
+            resident = cus * per_cu;
+        else
+            resident = 2048;
+    }
+    const int blocks = nstrips < resident ? nstrips : resident;
     hipLaunchKernelGGL((dcte_fix_strips<N, BPP, SEM>), dim3(blocks), dim3(64), 0, s, p);
     return hipGetLastError();
 }
