@@ -59,7 +59,8 @@ def parse(argv=None):
                          "(N * size) x size frame")
     ap.add_argument("--check", action="store_true",
                     help="after timing, recompute every band from regenerated rows (no "
-                         "exchange) and require bit-equality")
+                         "exchange) and require bit-equality (default on for --gpus > 1)")
+    ap.add_argument("--no-check", action="store_true", help="skip that check for --gpus > 1")
     ap.add_argument("--cpu-rehearsal", action="store_true",
                     help="no GPU: launch the ranks, split a --size frame into bands and "
                          "exchange the halos over gloo on CPU tensors, check them against "
@@ -384,7 +385,7 @@ def main():
     valu_rate = (px_per_rank * valu_per_px / (kernel_ms_per_step * 1e-3)) if valu_per_px else None
 
     check = None
-    if args.check:
+    if args.check or (world > 1 and not args.no_check):
         # regenerate this band's rows INCLUDING the halo rows straight from the
         # global frame definition and recompute without any exchange
         ref_in = synth.natural_rows(band.row0, band.rows, W, 3, seed=0, device=dev)
