@@ -229,15 +229,17 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
     // decision + store (+ refinement flag) of output pixel (x, y)
     auto emit = [&](int y, int xx, float mt, float me) {
         if (xx >= w) return;
-        const bool edge = me > mt;                  // selects, not fmaxf/fminf: no canonicalising ops
-        const float hi = edge ? me : mt, lo = edge ? mt : me;
+        const bool edge = me > mt;
+        // the product, then the select (the weights stay in SGPRs)
+        const float e_out = me * we, t_out = mt * wt;
         // row offset is wave-uniform (soffset), column offset per lane
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hi * (edge ? we : wt)), orsrc,
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(edge ? e_out : t_out), orsrc,
                                               xx * 4, (y - ys) * ostride4, 0);
-        // refine in fp64 when the class is uncertain: lo within the fp32
-        // error band of hi (never for all-zero windows); every pixel when
-        // tie_tau >= 1 (testing)
-        if ((check_ties && lo > keep * hi) || force_all) {
+        // refine in fp64 when the class is uncertain: the smaller maximum
+        // within the fp32 error band of the larger, lo > (1 - tau) hi, i.e.
+        // me > keep mt AND mt > keep me (never for all-zero windows); every
+        // pixel when tie_tau >= 1 (testing)
+        if ((check_ties && me > keep * mt && mt > keep * me) || force_all) {
             const unsigned k = atomicAdd(&nflag[sc], 1u);      // < 64 * tile_h
             strip_list[k] = (unsigned)((y - ys) * 64 + (xx - sx0));
         }
@@ -305,7 +307,17 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
             constexpr int u = decltype(U)::value;
             const int i = g * G + u;
             if (i < n_in) {
-                row_pass<N>(&lum[b][u][0], c, lane_p, ring[u % N]);
+                if constexpr (N == 8) {
+                    // the lane's row base, opaque to the optimiser: its 8 reads
+                    // then pair into ds_read2 off ONE base (offsets 0..7)
+                    // instead of one address add per pair
+                    using lds_cfloat = const __attribute__((address_space(3))) float;
+                    uint32_t a = (uint32_t)(uintptr_t)(lds_cfloat*)&lum[b][u][c];
+                    asm volatile("" : "+v"(a));
+                    row_pass<N>((const float*)(lds_cfloat*)(uintptr_t)a, 0, lane_p, ring[u % N]);
+                } else {
+                    row_pass<N>(&lum[b][u][0], c, lane_p, ring[u % N]);
+                }
                 if (i >= N - 1) {
                     float mt, me;
                     Cols<N>::template run<(u + 1) % N>(ring, lane_p, mt, me);
