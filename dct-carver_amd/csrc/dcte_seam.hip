@@ -42,32 +42,28 @@ __device__ __forceinline__ void seam_span(const int* __restrict__ seam, int w, i
 
 constexpr unsigned kRawBufFlags = 0x00020000u;   // gfx9 raw buffer dword3 (as dcte_map)
 constexpr int kShiftThreads = 256;
-#ifndef DCTE_SHIFT_DW
-#define DCTE_SHIFT_DW 8                     // A/B 4 / 8 / 16: 0.499 / 0.491 / 0.488 ms per 16384^2 step
+#ifndef DCTE_SHIFT_VEC
+#define DCTE_SHIFT_VEC 2                    // 16-byte blocks per thread per pass (8 KB per pass)
 #endif
-constexpr int kShiftDw = DCTE_SHIFT_DW;             // dwords per thread per pass
-
-// 4 bytes at byte offset `off` (any alignment) of a buffer resource: two
-// aligned dword loads + a byte funnel shift (out-of-range dwords read 0)
-__device__ __forceinline__ uint32_t load4(__amdgpu_buffer_rsrc_t r, uint32_t off)
-{
-    const uint32_t a = off & ~3u, sh = off & 3u;
-    const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(r, (int)a, 0, 0);
-    const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(a + 4u), 0, 0);
-    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * sh));
-}
+constexpr int kShiftVec = DCTE_SHIFT_VEC;
 
 // One workgroup per row.  New row bytes [o0, o1) come from old byte
 // b + (b >= s*bpp ? bpp : 0); new map entries x come from old x (left of the
-// recomputed band) or x + 1 (right of it).  INPLACE (px_out == px, same row
-// stride; map likewise): only the part right of the seam moves (o0 = s*bpp),
-// every pass loads all its sources before the barrier and stores after it,
-// and a pass never reads bytes an earlier pass wrote (sources lie at or
-// right of the destinations); the <= 3 unaligned head bytes are loaded first
-// and the <= 3 tail bytes (read as sources by the last dwords) are stored last.
+// recomputed band) or x + 1 (right of it).  Both move in 16-byte destination
+// blocks: a frame block's 16 source bytes (any alignment) are one dwordx4 +
+// one dword from the aligned dword below them, funnel-shifted
+// (v_alignbyte); a map block's 4 source floats are one dword-aligned
+// dwordx4.  INPLACE (px_out == px, same row stride; map likewise): only the
+// part right of the seam moves (o0 = s*bpp), every pass loads all its sources
+// before the barrier and stores after it, and a pass never reads bytes an
+// earlier pass wrote (sources lie at or right of the destinations); the
+// <= 15 unaligned head bytes (<= 3 head floats) are loaded first and the
+// <= 15 tail bytes (<= 3 floats), read as sources by the last blocks, are
+// stored last.
 template <int BPP, bool INPLACE>
 __global__ __launch_bounds__(kShiftThreads) void dcte_seam_shift(const SeamParams p)
 {
+    using u4 = unsigned int __attribute__((ext_vector_type(4)));
     const int y = blockIdx.x;
     const int tx = threadIdx.x;
     const int w = p.w, w1 = w - 1;
@@ -79,9 +75,9 @@ __global__ __launch_bounds__(kShiftThreads) void dcte_seam_shift(const SeamParam
     // ---- frame bytes
     const uintptr_t ib = reinterpret_cast<uintptr_t>(p.px);
     const uint32_t iofs = (uint32_t)(ib & 3u);
-    // records rounded up to whole dwords: buffer loads are range-checked per
-    // dword, and the aligned dword holding the frame's last byte never
-    // crosses a page, so it is always mapped
+    // records rounded up to whole dwords: every load below lies inside them
+    // (a block's sources end at most at the row's end), and the aligned
+    // dword holding the frame's last byte never crosses a page
     const uint32_t nrec =
         (iofs + (uint32_t)((long long)(p.h - 1) * p.rowstride) + (uint32_t)(w * BPP) + 3u) & ~3u;
     __amdgpu_buffer_rsrc_t in = __builtin_amdgcn_make_buffer_rsrc(
@@ -91,43 +87,63 @@ __global__ __launch_bounds__(kShiftThreads) void dcte_seam_shift(const SeamParam
     const int sb = s * BPP;
     const int o0 = INPLACE ? sb : 0, o1 = w1 * BPP;
     auto src = [&](int b) -> uint32_t { return irow + (uint32_t)(b + (b >= sb ? BPP : 0)); };
-    // aligned dword span [d0, d1) of the destination row, head [o0, d0), tail [d1, o1)
-    const int mis = (int)(reinterpret_cast<uintptr_t>(orow) & 3u);
-    int d0 = o0 + ((4 - ((mis + o0) & 3)) & 3);
+    // 16 bytes starting at byte q of `in`
+    auto load16 = [&](uint32_t q) -> u4 {
+        const uint32_t a = q & ~3u, sh = q & 3u;
+        const u4 v = __builtin_amdgcn_raw_buffer_load_b128(in, (int)a, 0, 0);
+        const uint32_t e = __builtin_amdgcn_raw_buffer_load_b32(in, (int)(a + 16u), 0, 0);
+        u4 r;
+        r.x = __builtin_amdgcn_alignbyte(v.y, v.x, sh);
+        r.y = __builtin_amdgcn_alignbyte(v.z, v.y, sh);
+        r.z = __builtin_amdgcn_alignbyte(v.w, v.z, sh);
+        r.w = __builtin_amdgcn_alignbyte(e, v.w, sh);
+        return r;
+    };
+    // 16-byte-aligned destination blocks [d0, d1), head [o0, d0), tail [d1, o1)
+    const int mis = (int)(reinterpret_cast<uintptr_t>(orow) & 15u);
+    int d0 = o0 + ((16 - ((mis + o0) & 15)) & 15);
     if (d0 > o1) d0 = o1;
-    int d1 = d0 + ((o1 - d0) & ~3);
-    uint8_t edge_v = 0;                               // one head/tail byte per thread < 6
+    const int d1 = d0 + ((o1 - d0) & ~15);
+    uint8_t edge_v = 0;                               // one head/tail byte per thread < 30
     int edge_b = -1;
-    if (tx < 3 && o0 + tx < d0) edge_b = o0 + tx;
-    if (tx >= 3 && tx < 6 && d1 + (tx - 3) < o1) edge_b = d1 + (tx - 3);
+    if (tx < 15 && o0 + tx < d0) edge_b = o0 + tx;
+    if (tx >= 15 && tx < 30 && d1 + (tx - 15) < o1) edge_b = d1 + (tx - 15);
     if (edge_b >= 0) edge_v = (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(in, (int)src(edge_b), 0, 0);
-    for (int base = d0; base < d1; base += 4 * kShiftThreads * kShiftDw) {
-        uint32_t v[kShiftDw];
+    for (int base = d0; base < d1; base += 16 * kShiftThreads * kShiftVec) {
+        u4 v[kShiftVec];
 #pragma unroll
-        for (int k = 0; k < kShiftDw; k++) {
-            const int b = base + 4 * (tx + k * kShiftThreads);
-            v[k] = 0;
+        for (int k = 0; k < kShiftVec; k++) {
+            const int b = base + 16 * (tx + k * kShiftThreads);
+            v[k] = u4{0u, 0u, 0u, 0u};
             if (b < d1) {
-                if (b + 4 <= sb || b >= sb) {
-                    v[k] = load4(in, src(b));
-                } else {                                   // dword straddling the seam
+                if (INPLACE || b >= sb) {
+                    v[k] = load16(irow + (uint32_t)(b + BPP));
+                } else if (b + 16 <= sb) {
+                    v[k] = load16(irow + (uint32_t)b);
+                } else {                                   // the block straddling the seam
+                    uint32_t d[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-                    for (int j = 0; j < 4; j++)
-                        v[k] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(in, (int)src(b + j), 0, 0) << (8 * j);
+                    for (int j = 0; j < 16; j++)
+                        d[j >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(in, (int)src(b + j), 0, 0)
+                                     << (8 * (j & 3));
+                    v[k] = u4{d[0], d[1], d[2], d[3]};
                 }
             }
         }
         if constexpr (INPLACE) __syncthreads();
 #pragma unroll
-        for (int k = 0; k < kShiftDw; k++) {
-            const int b = base + 4 * (tx + k * kShiftThreads);
-            if (b < d1) *reinterpret_cast<uint32_t*>(orow + b) = v[k];
+        for (int k = 0; k < kShiftVec; k++) {
+            const int b = base + 16 * (tx + k * kShiftThreads);
+            if (b < d1) *reinterpret_cast<u4*>(orow + b) = v[k];
         }
     }
 
     // ---- map: rows of floats (4-byte aligned)
     const float* mrow = p.map + (long long)y * p.map_stride;
     float* nrow = p.map_out + (long long)y * p.map_out_stride;
+    // the source row through a buffer resource: dword-aligned dwordx4 loads
+    __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(mrow), (short)0,
+                                                                   w * 4, (int)kRawBufFlags);
     // left part [0, lo - HR) keeps x; right part [r0, w1) takes x + 1
     const int lend = max(0, min(w1, lo - HR));
     int r0 = hi + HL;                                  // first x with min(x - HL, w - 2) >= hi
@@ -136,22 +152,33 @@ __global__ __launch_bounds__(kShiftThreads) void dcte_seam_shift(const SeamParam
     if constexpr (!INPLACE) {
         for (int x = tx; x < lend; x += kShiftThreads) nrow[x] = mrow[x];
     }
-    for (int base = r0; base < w1; base += kShiftThreads * kShiftDw) {
-        float v[kShiftDw];
+    // 4-float destination blocks [x0, x1) (16-byte aligned), head [r0, x0), tail [x1, w1)
+    const int mmis = (int)((reinterpret_cast<uintptr_t>(nrow) >> 2) & 3u);
+    int x0 = r0 + ((4 - ((mmis + r0) & 3)) & 3);
+    if (x0 > w1) x0 = w1;
+    const int x1 = x0 + ((w1 - x0) & ~3);
+    float medge_v = 0.0f;                              // one head/tail float per thread in [32, 38)
+    int medge_x = -1;
+    if (tx >= 32 && tx < 35 && r0 + (tx - 32) < x0) medge_x = r0 + (tx - 32);
+    if (tx >= 35 && tx < 38 && x1 + (tx - 35) < w1) medge_x = x1 + (tx - 35);
+    if (medge_x >= 0) medge_v = mrow[medge_x + 1];
+    for (int base = x0; base < x1; base += 4 * kShiftThreads * kShiftVec) {
+        u4 v[kShiftVec];
 #pragma unroll
-        for (int k = 0; k < kShiftDw; k++) {
-            const int x = base + tx + k * kShiftThreads;
-            v[k] = x < w1 ? mrow[x + 1] : 0.0f;
+        for (int k = 0; k < kShiftVec; k++) {
+            const int x = base + 4 * (tx + k * kShiftThreads);
+            v[k] = x < x1 ? __builtin_amdgcn_raw_buffer_load_b128(mr, (x + 1) * 4, 0, 0) : u4{0u, 0u, 0u, 0u};
         }
         if constexpr (INPLACE) __syncthreads();
 #pragma unroll
-        for (int k = 0; k < kShiftDw; k++) {
-            const int x = base + tx + k * kShiftThreads;
-            if (x < w1) nrow[x] = v[k];
+        for (int k = 0; k < kShiftVec; k++) {
+            const int x = base + 4 * (tx + k * kShiftThreads);
+            if (x < x1) *reinterpret_cast<u4*>(nrow + x) = v[k];
         }
     }
     if constexpr (INPLACE) __syncthreads();
     if (edge_b >= 0) orow[edge_b] = edge_v;
+    if (medge_x >= 0) nrow[medge_x] = medge_v;
 }
 
 __device__ __forceinline__ void emit_pixel(const SeamParams& p, float mt, float me, float* dst,
