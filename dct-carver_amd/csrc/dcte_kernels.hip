@@ -635,7 +635,7 @@ struct FixStrip {
     static constexpr int LW = 64 + N - 1;             // luma columns of a strip
     static constexpr int G = Geo<N, SEM>::G;          // map kernel rows per group
 #ifndef DCTE_FIX_GPS
-#define DCTE_FIX_GPS 2   // A/B 1 vs 2 at N = 8: line art -6 % (grey) / -1 % (RGB), 8-px grid -10 %
+#define DCTE_FIX_GPS 2   // A/B at N = 8 vs 1: line art -6 % (grey) / -1 % (RGB), 8-px grid -10 %; 3, 4: +20-50 % (profiles/r02/fix_gps_ab.jsonl)
 #endif
     static constexpr int GPS = N == 16 ? 1 : DCTE_FIX_GPS;   // map row groups per band
     static constexpr int SBH = GPS * G;               // output rows per band (16; N = 16: 16)
