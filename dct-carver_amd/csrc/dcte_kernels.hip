@@ -658,14 +658,12 @@ __device__ __forceinline__ unsigned wave_max_u(unsigned v)
 // the lum index of window element (0, 0); w holds N rows of N + 1 doubles
 // (the pad keeps both passes' accesses on distinct LDS banks).  Every lane
 // of the wave calls it.
-template <int N, int SEM>
-__device__ __forceinline__ void refine_group(const double* lum, int LW, int at, double* w, int l,
-                                             double& best, bool& edge)
+template <int N, class Line>
+__device__ __forceinline__ void refine_group_f(Line&& line, double* w, int l, double& best, bool& edge)
 {
     double v[N];
 #pragma unroll
-    for (int i = 0; i < N; i++)   // d[i][l]: liblqr data[dx][dy] (row l, column i); preview data[dy][dx]
-        v[i] = SEM == kSemLqr ? lum[at + l * LW + i] : lum[at + i * LW + l];
+    for (int i = 0; i < N; i++) v[i] = line(i);
     if constexpr (N == 8) r64::step8(v, 1); else r64::step16(v, 1);
 #pragma unroll
     for (int i = 0; i < N; i++) w[i * (N + 1) + l] = v[i];   // rows padded: no bank conflicts
@@ -675,6 +673,15 @@ __device__ __forceinline__ void refine_group(const double* lum, int LW, int at, 
     wave_sync_lds();                                   // w may be refilled after this
     if constexpr (N == 8) r64::step8(v, 1); else r64::step16(v, 1);
     lastmax_group<N>(v, l, best, edge);
+}
+
+template <int N, int SEM>
+__device__ __forceinline__ void refine_group(const double* lum, int LW, int at, double* w, int l,
+                                             double& best, bool& edge)
+{
+    // d[i][l]: liblqr data[dx][dy] (row l, column i); preview data[dy][dx]
+    refine_group_f<N>([&](int i) { return SEM == kSemLqr ? lum[at + l * LW + i] : lum[at + i * LW + l]; },
+                      w, l, best, edge);
 }
 
 template <int N, int BPP, int SEM>
@@ -688,20 +695,31 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
     constexpr int PDW = PB / 4;
     constexpr bool kGroup = N >= 8;                    // N lanes per pixel (else one lane)
     constexpr int PPW = kGroup ? 64 / N : 64;          // pixels per wave pass
+#ifndef DCTE_FIX_OTF
+#define DCTE_FIX_OTF 1
+#endif
+    // kOtf (grey layers): window elements converted from the band's raw bytes
+    // as they are read -- one byte and one table read each -- instead of a
+    // staged fp64 luma band: fewer LDS bytes, more waves per CU (line art
+    // N = 8: 1.02 -> 0.67 ms, N = 16: 1.28 -> 0.96; profiles/r02/fix_otf_ab.jsonl).
+    // RGB keeps the staged band: three bytes, three table reads and five fp64
+    // operations per element read would cost more than the occupancy wins
+    // (N = 16: 1.66 -> 1.93 ms).
+    constexpr bool kOtf = DCTE_FIX_OTF && BPP == 1;
     __shared__ double lut[256];
-    __shared__ double lum[LR * LW];                    // fp64 luma of one band (+ halo), needed columns
+    __shared__ double lum[kOtf ? 1 : LR * LW];         // fp64 luma of one band (+ halo), needed columns
     __shared__ unsigned char mis[LR];                  // byte offset of each raw row's first pixel
-    __shared__ unsigned char colidx[LW];               // the needed luma columns, ascending
+    __shared__ unsigned char colidx[kOtf ? 1 : LW];    // the needed luma columns, ascending
     // per group: N rows of N + 1 doubles, plus a pad that starts consecutive
     // groups 16 banks apart
     constexpr int WS = kGroup ? (N * (N + 1) + 7) / 8 * 8 + 8 : 1;
-    // the band's raw rows and the groups' window buffers share one region:
-    // raw is read only by the luma conversion, the windows only after it
-    // (fewer LDS bytes per wave, more waves per CU)
+    // the band's raw rows and the groups' window buffers: one region when raw
+    // is read only by the luma conversion (the windows only after it)
     constexpr int RAW_D = (LR * PDW + 1) / 2, WIN_D = (kGroup ? PPW : 1) * WS;
-    __shared__ __attribute__((aligned(16))) double rw_lds[RAW_D > WIN_D ? RAW_D : WIN_D];
+    constexpr int RW_D = kOtf ? RAW_D + WIN_D : (RAW_D > WIN_D ? RAW_D : WIN_D);
+    __shared__ __attribute__((aligned(16))) double rw_lds[RW_D];
     uint32_t* const raw = reinterpret_cast<uint32_t*>(rw_lds);
-    double (*const win)[WS] = reinterpret_cast<double (*)[WS]>(rw_lds);
+    double (*const win)[WS] = reinterpret_cast<double (*)[WS]>(rw_lds + (kOtf ? RAW_D : 0));
     const MapParams& p = tp.m;
     const unsigned ndirty = *p.dirty_count;
     constexpr int SB = kGroup ? PPW : 8;               // strips per batch (below)
@@ -858,6 +876,13 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
             const bool interior = sx0 - HL >= 0 && (sx0 - HL + LW) * BPP + 3 <= p.w * BPP;
             constexpr int SPAN = LW * BPP;
             constexpr int U = (LR * PDW + 63) / 64;
+            // fp64 luma of band row r, span column c
+            auto lum_at = [&](int r, int c) -> double {
+                if constexpr (kOtf)
+                    return luma(reinterpret_cast<const uint8_t*>(&raw[r * PDW]) + mis[r] + c * BPP);
+                else
+                    return lum[r * LW + c];
+            };
             auto band_rows = [&](int bb, int& r0, int& nrows) {
                 // band bb: output rows [max(A, 0), min(A + SBH, ye - ys)), A = bb SBH - (N - 1);
                 // input rows from r0 = max(A, 0) - HL (tile-relative)
@@ -868,6 +893,11 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
             uint32_t v[U];
             // raw dwords of band bb -> v (interior strips: every row's span is in
             // the frame); each row's misalignment -> mis
+            // byte offset of the span's first pixel in frame row gy
+            auto row_addr = [&](int gy) -> uint32_t {
+                return base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
+                       (uint32_t)((sx0 - HL) * BPP);
+            };
             auto issue_raw = [&](int bb) {
                 int r0, nrows;
                 band_rows(bb, r0, nrows);
@@ -878,9 +908,7 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
                     v[u] = 0;
                     if (r < nrows) {
                         const int gy = clampi(ys + r0 + r, 0, p.h - 1);
-                        const uint32_t a = base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
-                                           (uint32_t)((sx0 - HL) * BPP);
-                        if (dw == 0) mis[r] = (unsigned char)(a & 3u);
+                        const uint32_t a = row_addr(gy);
                         if (dw * 4 < (int)(a & 3u) + SPAN)
                             v[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)((a & ~3u) + 4u * dw), 0, 0);
                     }
@@ -926,7 +954,15 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
 #pragma unroll
                     for (int u = 0; u < U; u++) {
                         const int e = lane + 64 * u;
-                        if (e < nrows * PDW) raw[e] = v[u];
+                        if (e < nrows * PDW) {
+                            raw[e] = v[u];
+                            // each row's misalignment, written with its bytes (the
+                            // next band's loads are issued while this band's
+                            // windows still read mis)
+                            const int r = e / PDW;
+                            if (e == r * PDW)
+                                mis[r] = (unsigned char)(row_addr(clampi(ys + r0 + r, 0, p.h - 1)) & 3u);
+                        }
                     }
                 } else {
                     for (int e = lane; e < nrows * LW; e += 64) {
@@ -938,6 +974,7 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
                         if (c == 0) mis[r] = 0;
                     }
                 }
+                if constexpr (!kOtf) {
                 // the needed columns, compacted
                 const int n0 = __popc(m0), n1 = __popc(m1);
                 const int ncols = n0 + n1 + __popc(m2);
@@ -976,6 +1013,7 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
 #pragma unroll
                     for (int k = 0; k < kConv; k++) lum[at[k] * LW + cc[k]] = lv[k];
                 }
+                }   // !kOtf
                 wave_sync_lds();
                 // the next run's band: its raw rows in flight through this band's compute
                 int bN = b;
@@ -988,7 +1026,6 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
                     for (unsigned q = pos + lane; q < end; q += 64) {
                         const unsigned lc = single ? loc0 : list[q];
                         const int ly = (int)(lc >> 6), lx = (int)(lc & 63);
-                        const double* base = &lum[(ly - HL - r0) * LW + lx];
                         double d[N * N];
 #pragma unroll
                         for (int i = 0; i < N; i++)
@@ -996,7 +1033,7 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
                             for (int j = 0; j < N; j++) {
                                 int ox, oy;
                                 offs(i, j, ox, oy);
-                                d[i * N + j] = base[oy * LW + ox];
+                                d[i * N + j] = lum_at(ly - HL - r0 + oy, lx + ox);
                             }
                         double m;
                         bool edge;
@@ -1013,7 +1050,15 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
                         const int ly = (int)(lc >> 6), lx = (int)(lc & 63);
                         double best;
                         bool edge;
-                        refine_group<N, SEM>(lum, LW, (ly - HL - r0) * LW + lx, win[grp], l, best, edge);
+                        const int rr = ly - HL - r0;
+                        if constexpr (kOtf) {
+                            // liblqr: lane l reads window row l; preview: window column l
+                            refine_group_f<N>([&](int i) {
+                                return SEM == kSemLqr ? lum_at(rr + l, lx + i) : lum_at(rr + i, lx + l);
+                            }, win[grp], l, best, edge);
+                        } else {
+                            refine_group<N, SEM>(lum, LW, rr * LW + lx, win[grp], l, best, edge);
+                        }
                         if (valid && l == 0) store(lx, ly, best, edge);
                     }
                 }
