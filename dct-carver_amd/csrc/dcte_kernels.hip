@@ -705,8 +705,16 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
     // RGB keeps the staged band: three bytes, three table reads and five fp64
     // operations per element read would cost more than the occupancy wins
     // (N = 16: 1.66 -> 1.93 ms).
-    constexpr bool kOtf = DCTE_FIX_OTF && BPP == 1;
-    __shared__ double lut[256];
+#ifndef DCTE_FIX_OTF_RGB
+#define DCTE_FIX_OTF_RGB 1
+#endif
+    // liblqr RGB at N = 8 reads elements from the raw band too, with the three
+    // weighted quotients k_c (v / 255) tabulated so a luma is two fp64 adds
+    // ((k_r r + k_g g) + k_b b, the reference's order): line art RGB 1.41 ->
+    // 1.33 ms; at N = 16 the same costs +30 % (profiles/r02/fix_otf_ab.jsonl)
+    constexpr bool kTab = DCTE_FIX_OTF_RGB && SEM == kSemLqr && BPP == 3 && N == 8;
+    constexpr bool kOtf = DCTE_FIX_OTF && (BPP == 1 || kTab);
+    __shared__ double lut[kTab ? 3 * 256 : 256];
     __shared__ double lum[kOtf ? 1 : LR * LW];         // fp64 luma of one band (+ halo), needed columns
     __shared__ unsigned char mis[LR];                  // byte offset of each raw row's first pixel
     __shared__ unsigned char colidx[kOtf ? 1 : LW];    // the needed luma columns, ascending
@@ -726,7 +734,17 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
     if (blockIdx.x * SB >= ndirty) return;             // uniform
     const int lane = threadIdx.x;
 #pragma unroll
-    for (int t = 0; t < 4; t++) lut[lane + 64 * t] = (double)(lane + 64 * t) / 255;
+    for (int t = 0; t < 4; t++) {
+        const int v = lane + 64 * t;
+        const double q = (double)v / 255;
+        if constexpr (kTab) {
+            lut[v] = 0.2126 * q;
+            lut[256 + v] = 0.7152 * q;
+            lut[512 + v] = 0.0722 * q;
+        } else {
+            lut[v] = q;
+        }
+    }
     wave_sync_lds();
 
     // the frame through a bounds-checked buffer resource (as dcte_map)
@@ -742,6 +760,7 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
     auto luma = [&](const uint8_t* q) -> double {
         if constexpr (SEM == kSemLqr) {
             if constexpr (BPP == 1) return lut[q[0]];
+            else if constexpr (kTab) return lut[q[0]] + lut[256 + q[1]] + lut[512 + q[2]];
             else return 0.2126 * lut[q[0]] + 0.7152 * lut[q[1]] + 0.0722 * lut[q[2]];
         } else {
             return (double)preview_luma(q[0], BPP > 1 ? q[1] : 0u, BPP > 1 ? q[2] : 0u, BPP);
