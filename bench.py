@@ -315,12 +315,17 @@ def main():
     i0, i1 = band.interior()
     row0 = band.row0
 
-    def run_rows(y0, y1):
+    def run_rows(y0, y1, st=stream):
         if y1 <= y0:
             return
         ctx.energy_map_device(buf.data_ptr(), buf.stride(0), W, H, 3, row0, band.rows, y0, y1,
-                              n, e, t, out[y0 - band.Y0:].data_ptr(), out.stride(0), stream,
+                              n, e, t, out[y0 - band.Y0:].data_ptr(), out.stride(0), st,
                               dev_index)
+
+    # halo-dependent edge rows on a stream of their own: they wait for the
+    # halos only, so they run beside the interior instead of after it
+    # (tools/band_split.py: 8 -> 2 us of split overhead per 2048-row band)
+    edge_stream = torch.cuda.Stream(dev) if world > 1 and not gloo else None
 
     host_buf = torch.empty(buf.shape, dtype=torch.uint8, pin_memory=True) if world > 1 and gloo else None
 
@@ -338,13 +343,21 @@ def main():
                 buf[:band.top].copy_(host_buf[:band.top], non_blocking=True)
             if band.bot:
                 buf[band.rows - band.bot:].copy_(host_buf[band.rows - band.bot:], non_blocking=True)
+            for a, b in band.edges():
+                run_rows(a, b)
+        elif edge_stream is not None:
+            reqs = D.exchange_halos(buf, band)   # after this rank's previous step (incl. its edges)
+            run_rows(i0, i1)                     # overlaps the exchange
+            with torch.cuda.stream(edge_stream):
+                for r in reqs:
+                    r.wait()                     # the edge stream waits for the halos
+                for a, b in band.edges():
+                    run_rows(a, b, edge_stream.cuda_stream)
+            torch.cuda.current_stream(dev).wait_stream(edge_stream)
         else:
-            reqs = D.exchange_halos(buf, band) if world > 1 else []
-            run_rows(i0, i1)                # overlaps the exchange
-            for r in reqs:
-                r.wait()                    # current stream waits for the halos
-        for a, b in band.edges():
-            run_rows(a, b)
+            run_rows(i0, i1)
+            for a, b in band.edges():
+                run_rows(a, b)
 
     for _ in range(args.warmup):
         step()
