@@ -249,11 +249,15 @@ class Context:
         return out
 
     def energy_image_u8(self, px, n=8, edges=0.5, textures=0.5, mode=DCTE_NORM_LQR, channels=1,
-                        semantics=DCTE_LQR):
+                        semantics=DCTE_LQR, out=None):
         px = np.ascontiguousarray(px, dtype=np.uint8)
         h, w = px.shape[:2]
         bpp = 1 if px.ndim == 2 else px.shape[2]
-        out = np.empty((h, w) + ((channels,) if channels > 1 else ()), np.uint8)
+        shape = (h, w) + ((channels,) if channels > 1 else ())
+        if out is None:
+            out = np.empty(shape, np.uint8)
+        elif out.shape != shape or out.dtype != np.uint8 or not out.flags.c_contiguous:
+            raise ValueError(f"out must be a C-contiguous uint8 array of shape {shape}")
         self._check(lib().dcte_energy_image_u8(self._h, px.ctypes.data, w, h, bpp, _rowstride(px),
                                                n, edges, textures, semantics, mode, channels,
                                                out.ctypes.data))

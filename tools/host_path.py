@@ -74,6 +74,11 @@ def main():
         res.append({"case": "dcte_energy_image_u8 host->host (pageable, fresh output array per call)",
                     "ms": round(med * 1e3, 2),
                     "mpx_s": round(mpx / med, 1)})
+        u8 = np.empty((S, S), np.uint8)
+        med, best = timed(lambda: ctx.energy_image_u8(px_np, a.n, 0.3, 0.7, out=u8), a.iters)
+        res.append({"case": "dcte_energy_image_u8 host->host (pageable, output array reused)",
+                    "ms": round(med * 1e3, 2),
+                    "mpx_s": round(mpx / med, 1)})
     # bare copy rates of the same bytes (torch, same stream semantics)
     for name, fn, nbytes in (
             ("H2D pageable frame", lambda: dev.copy_(torch.from_numpy(px_np)), px_np.nbytes),
