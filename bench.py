@@ -61,6 +61,11 @@ def parse(argv=None):
                     help="after timing, recompute every band from regenerated rows (no "
                          "exchange) and require bit-equality (default on for --gpus > 1)")
     ap.add_argument("--no-check", action="store_true", help="skip that check for --gpus > 1")
+    ap.add_argument("--shared-gpu", action="store_true",
+                    help="RCCL rehearsal on a box with fewer GPUs than ranks: the self-launched "
+                         "ranks get distinct NCCL_HOSTIDs so RCCL accepts several ranks on one "
+                         "device (halos then travel over its socket transport on loopback "
+                         "instead of xGMI; the RCCL code path itself is the one measured runs use)")
     ap.add_argument("--cpu-rehearsal", action="store_true",
                     help="no GPU: launch the ranks, split a --size frame into bands and "
                          "exchange the halos over gloo on CPU tensors, check them against "
@@ -76,7 +81,20 @@ def free_port():
         return s.getsockname()[1]
 
 
-def launch_ranks(n, argv):
+def rank_env(r, n, port, shared_gpu=False):
+    """Environment of rank r of n.  shared_gpu: RCCL refuses two ranks on one
+    device of one host ("Duplicate GPU detected"); a distinct NCCL_HOSTID per
+    rank makes each rank its own host, so RCCL connects them through its net
+    transport (sockets on loopback, no InfiniBand)."""
+    env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+               LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if shared_gpu:
+        env.update(NCCL_HOSTID=f"dcte-rehearsal-rank{r}", NCCL_SOCKET_IFNAME="lo",
+                   NCCL_IB_DISABLE="1")
+    return env
+
+
+def launch_ranks(n, argv, shared_gpu=False):
     """Start n rank processes of this script (RANK/LOCAL_RANK/WORLD_SIZE and a
     127.0.0.1 rendezvous in their environment) and wait for them.  Runs before
     this process touches a GPU; children are started, never exec'd into.
@@ -84,8 +102,7 @@ def launch_ranks(n, argv):
     port = free_port()
     procs = []
     for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env = rank_env(r, n, port, shared_gpu)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
                                       env=env))
     rc = 0
@@ -261,7 +278,7 @@ def cpu_rehearsal(args):
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.shared_gpu))
 
     sys.path.insert(0, os.path.join(ROOT, "dct-carver_amd"))
     if args.cpu_rehearsal:
@@ -280,6 +297,11 @@ def main():
         print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         sys.exit(2)
     ndev = torch.cuda.device_count()
+    if world > ndev and args.dist_backend == "nccl" and not args.shared_gpu:
+        print(f"bench: {world} ranks but {ndev} GPU(s): RCCL needs one device per rank "
+              f"(--shared-gpu rehearses RCCL with ranks sharing a device, --dist-backend gloo "
+              f"stages halos through host memory)", file=sys.stderr)
+        sys.exit(2)
     gpu = local % max(1, ndev)          # == local on a full node
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
@@ -469,8 +491,11 @@ def main():
             res["check_bands_bit_exact"] = check
         if world > 1 and gloo:
             res["config"]["parallelism"] += " (halo via gloo rehearsal)"
-            if ndev < world:
-                res["config"]["parallelism"] += f"; {world} ranks share {ndev} GPU(s)"
+        if world > 1 and not gloo and args.shared_gpu:
+            res["config"]["parallelism"] += (" (RCCL rehearsal: distinct NCCL_HOSTID per rank, "
+                                             "halos over RCCL's socket transport on loopback)")
+        if world > 1 and ndev < world:
+            res["config"]["parallelism"] += f"; {world} ranks share {ndev} GPU(s)"
         if world == 1 and not args.no_host_path:
             res["host_path"] = host_path(ctx, buf, n, e, t)
         if world == 1 and not args.no_cpu_baseline:
