@@ -392,18 +392,20 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    enqueued = time.perf_counter() - t0       # host time to issue the K steps
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     launches, kern_ms = ctx.profile_read()
     ctx.set_option(dctenergy.DCTE_OPT_PROFILE, 0)
-    stats = torch.tensor([elapsed, kern_ms / args.steps], dtype=torch.float64,
+    stats = torch.tensor([elapsed, kern_ms / args.steps, enqueued], dtype=torch.float64,
                          device="cpu" if gloo else dev)
     if world > 1:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
     elapsed = float(stats[0])
     kernel_ms_max_rank = float(stats[1])
+    host_ms_per_step = float(stats[2]) * 1e3 / args.steps
 
     px_per_rank = band.own * W
     total_px = H * W if strong else px_per_rank * world
@@ -444,6 +446,9 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
+            # host time to ISSUE one step (max over ranks): near ms_per_step
+            # means the launches, not the GPU, set the pace
+            "host_ms_per_step": round(host_ms_per_step, 4),
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,

@@ -628,6 +628,9 @@ __global__ __launch_bounds__(kFixThreads) void dcte_fix(const FixParams p)
 // (profiles/r02/fix_direct.jsonl).
 template <int N>
 constexpr unsigned kFixDirect = N == 16 ? 32u : 128u;
+#ifndef DCTE_FIX_PIPE
+#define DCTE_FIX_PIPE 1  // sparse strips (N = 8, 16): dword row fetches, next window in flight
+#endif
 
 template <int N, int SEM>
 struct FixStrip {
@@ -684,8 +687,15 @@ __device__ __forceinline__ void refine_group(const double* lum, int LW, int at, 
                       w, l, best, edge);
 }
 
+// grey layers at N <= 8 fit 128 VGPRs: 4 waves per SIMD (the LDS allows them)
+#ifndef DCTE_FIX_MINW
+#define DCTE_FIX_MINW 4
+#endif
+template <int N, int BPP>
+constexpr int kFixMinWaves = (BPP == 1 && N <= 8) ? DCTE_FIX_MINW : 1;
+
 template <int N, int BPP, int SEM>
-__global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
+__global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(const TileFixParams tp)
 {
     using FS = FixStrip<N, SEM>;
     constexpr int SPT = FS::SPT, LW = FS::LW, G = FS::G, SBH = FS::SBH, LR = FS::LR;
@@ -757,14 +767,17 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
 
     // liblqr luma of a pixel (src/render.c:315, LQR_ER_LUMA) [liblqr, unverified];
     // preview: the u8 RGB2LUMINANCE (src/render.h:5)
-    auto luma = [&](const uint8_t* q) -> double {
+    auto luma3 = [&](uint32_t c0, uint32_t c1, uint32_t c2) -> double {
         if constexpr (SEM == kSemLqr) {
-            if constexpr (BPP == 1) return lut[q[0]];
-            else if constexpr (kTab) return lut[q[0]] + lut[256 + q[1]] + lut[512 + q[2]];
-            else return 0.2126 * lut[q[0]] + 0.7152 * lut[q[1]] + 0.0722 * lut[q[2]];
+            if constexpr (BPP == 1) return lut[c0];
+            else if constexpr (kTab) return lut[c0] + lut[256 + c1] + lut[512 + c2];
+            else return 0.2126 * lut[c0] + 0.7152 * lut[c1] + 0.0722 * lut[c2];
         } else {
-            return (double)preview_luma(q[0], BPP > 1 ? q[1] : 0u, BPP > 1 ? q[2] : 0u, BPP);
+            return (double)preview_luma(c0, c1, c2, BPP);
         }
+    };
+    auto luma = [&](const uint8_t* q) -> double {
+        return luma3(q[0], BPP > 1 ? q[1] : 0u, BPP > 1 ? q[2] : 0u);
     };
     auto pixel = [&](int gx, int gy) {
         return p.px + (long long)(gy - p.in_row0) * p.rowstride + (long long)gx * BPP;
@@ -837,6 +850,91 @@ __global__ __launch_bounds__(64) void dcte_fix_strips(const TileFixParams tp)
                     refine_regs<N>(d, tp.ct, m, edge);
                     store_at(sg, lx, ly, m, edge);
                 }
+            }
+        } else if constexpr (DCTE_FIX_PIPE) {
+            // the group (GL = N lanes) takes its strip's entries one at a
+            // time, software-pipelined: entry i + 1's window bytes (and entry
+            // i + 2's list word) are in flight while entry i is transformed.
+            // Lane l fetches image row l of the window as whole dwords (the
+            // row's N pixels: 3 dwords grey, 7 RGB at N = 8) through the
+            // frame's buffer resource; windows clamped at the left / right
+            // frame border, or whose last dword would straddle the end of
+            // the readable bytes, gather per pixel instead (rare).
+            const int l = sl;
+            double* d = win[sgi];
+            constexpr int NW = (N * BPP + 3) / 4;              // dwords of a row's N pixels
+            constexpr int K = NW + 1;                          // loaded: any byte alignment
+            // One fetch buffer: entry i's bytes go to LDS first, then entry
+            // i + 1's loads are issued and fly while entry i is transformed.
+            // The loads are unconditional (an invalid or per-pixel entry
+            // reads past the buffer's end: zeros, no access), so the wait
+            // counts are the same on every path; list words are clamped
+            // into the strip's own entries.
+            uint32_t fv[K];
+            uint32_t foff = 0;
+            bool fwide = false;
+            auto list_at = [&](unsigned i) {
+                return sg.list[min(i, my_cnt > 0 ? my_cnt - 1 : 0u)];
+            };
+            auto fetch = [&](bool valid, unsigned loc) {
+                const int ly = (int)(loc >> 6), lx = (int)(loc & 63);
+                const int gx0 = sg.sx0 + lx - HL;
+                const int gy = clampi(sg.ys + ly + l - HL, 0, p.h - 1);
+                const uint32_t s = base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
+                                   (uint32_t)(gx0 * BPP);
+                fwide = valid && gx0 >= 0 && gx0 + N <= p.w && ((s + N * BPP - 1) | 3u) < nrec;
+                foff = s & 3u;
+                const uint32_t a = fwide ? (s & ~3u) : 0x7ffffff0u;     // past num_records: zeros
+#pragma unroll
+                for (int j = 0; j < K; j++)
+                    fv[j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * j), 0, 0);
+            };
+            unsigned lcur = list_at(0), lnext = list_at(1);
+            fetch(sparse && my_cnt > 0, lcur);
+            for (unsigned i = 0; i < smax; i++) {                         // uniform
+                const bool valid = sparse && i < my_cnt;
+                const int ly = (int)(lcur >> 6), lx = (int)(lcur & 63);
+                if (valid) {
+                    double lv[N];
+                    if (fwide) {
+                        uint32_t wd[NW];
+#pragma unroll
+                        for (int j = 0; j < NW; j++) wd[j] = __builtin_amdgcn_alignbyte(fv[j + 1], fv[j], foff);
+#pragma unroll
+                        for (int t = 0; t < N; t++) {
+                            auto byte = [&](int k) { return (wd[k >> 2] >> (8 * (k & 3))) & 255u; };
+                            lv[t] = luma3(byte(t * BPP), BPP > 1 ? byte(t * BPP + 1) : 0u,
+                                          BPP > 1 ? byte(t * BPP + 2) : 0u);
+                        }
+                    } else {
+                        const int gy = clampi(sg.ys + ly + l - HL, 0, p.h - 1);
+#pragma unroll
+                        for (int t = 0; t < N; t++)
+                            lv[t] = luma(pixel(clampi(sg.sx0 + lx + t - HL, 0, p.w - 1), gy));
+                    }
+                    // image row l, pixel t: liblqr data[t][l], preview data[l][t]
+#pragma unroll
+                    for (int t = 0; t < N; t++) d[SEM == kSemLqr ? t * (N + 1) + l : l * (N + 1) + t] = lv[t];
+                }
+                // entry i + 1's bytes and entry i + 2's list word in flight
+                const unsigned lafter = list_at(i + 2);
+                fetch(sparse && i + 1 < my_cnt, lnext);
+                wave_sync_lds();
+                // the group transforms its window in place (d[i][j] = d[i * (N + 1) + j])
+                if constexpr (N == 8) r64::step8(d + l, N + 1); else r64::step16(d + l, N + 1);
+                wave_sync_lds();
+                if constexpr (N == 8) r64::step8(d + (N + 1) * l, 1); else r64::step16(d + (N + 1) * l, 1);
+                wave_sync_lds();
+                double v[N];
+#pragma unroll
+                for (int c = 0; c < N; c++) v[c] = d[l * (N + 1) + c];
+                double best;
+                bool edge;
+                lastmax_group<N>(v, l, best, edge);
+                if (valid && l == 0) store_at(sg, lx, ly, best, edge);
+                wave_sync_lds();
+                lcur = lnext;
+                lnext = lafter;
             }
         } else {
             // the group (GL = N lanes) takes its strip's entries one at a

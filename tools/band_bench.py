@@ -10,6 +10,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "dct-carver_amd")]
@@ -48,14 +49,16 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize()
             e0.record(s)
+            h0 = time.perf_counter()
             for _ in range(a.iters):
                 for r in ranges:
                     run(*r)
+            host_ms = (time.perf_counter() - h0) * 1e3 / a.iters
             e1.record(s)
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / a.iters
             print(json.dumps({"pattern": name, "rows": R, "width": W, "n": n, "tile_h": a.tile_h,
-                              "ms_per_step": round(ms, 4),
+                              "ms_per_step": round(ms, 4), "host_ms_per_step": round(host_ms, 4),
                               "mpx_s": round(R * W / ms / 1e3, 1)}), flush=True)
 
 

@@ -41,7 +41,9 @@ def frames(S, torch, dev):
         "lineart_rgb": rgb(white(line)),
         "grid8_grey": white(grid8),
         "dots64_grey": torch.where(dots, 255, 16).to(torch.uint8),
+        "dots64_rgb": rgb(torch.where(dots, 255, 16).to(torch.uint8)),
         "text4_grey": white(text),
+        "text4_rgb": rgb(white(text)),
         "checker_grey": ((xx + yy) % 2 * 255).to(torch.uint8).expand(S, S).contiguous(),
     }
 
