@@ -628,6 +628,9 @@ __global__ __launch_bounds__(kFixThreads) void dcte_fix(const FixParams p)
 // (profiles/r02/fix_direct.jsonl).
 template <int N>
 constexpr unsigned kFixDirect = N == 16 ? 32u : 128u;
+#ifndef DCTE_FIX_ALIGNED
+#define DCTE_FIX_ALIGNED 1  // dense strips read the staged raw bytes as aligned dwords
+#endif
 #ifndef DCTE_FIX_PIPE
 #define DCTE_FIX_PIPE 1  // sparse strips (N = 8, 16): dword row fetches, next window in flight
 #endif
@@ -994,11 +997,46 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
             constexpr int SPAN = LW * BPP;
             constexpr int U = (LR * PDW + 63) / 64;
             // fp64 luma of band row r, span column c
+            // raw pixel (r, c) of the band: its bytes through the one or two
+            // ALIGNED dwords holding them (byte-wise reads got merged into
+            // unaligned 64-bit LDS reads: a third of the LDS cycles stalled)
+            auto px_at = [&](int r, int c) -> uint32_t {
+                const uint32_t o = (uint32_t)(r * PB) + mis[r] + (uint32_t)(c * BPP);
+                if constexpr (BPP == 1) {
+                    return reinterpret_cast<const uint8_t*>(raw)[o];
+                } else {
+                    const uint32_t lo = raw[o >> 2], hi = raw[(o >> 2) + 1];
+                    return __builtin_amdgcn_alignbyte(hi, lo, o & 3u);
+                }
+            };
+            auto luma_px = [&](uint32_t v) -> double {
+                return luma3(v & 255u, (v >> 8) & 255u, (v >> 16) & 255u);
+            };
             auto lum_at = [&](int r, int c) -> double {
                 if constexpr (kOtf)
-                    return luma(reinterpret_cast<const uint8_t*>(&raw[r * PDW]) + mis[r] + c * BPP);
+                    return DCTE_FIX_ALIGNED ? luma_px(px_at(r, c))
+                                            : luma(reinterpret_cast<const uint8_t*>(&raw[r * PDW]) + mis[r] + c * BPP);
                 else
                     return lum[r * LW + c];
+            };
+            // liblqr: the N pixels of band row r from column c on (a lane's
+            // window line) as whole aligned dwords
+            auto line_at = [&](int r, int c, double (&lv)[N]) {
+                constexpr int NW = (N * BPP + 3) / 4;
+                const uint32_t o = (uint32_t)(r * PB) + mis[r] + (uint32_t)(c * BPP);
+                const uint32_t* q = raw + (o >> 2);
+                uint32_t v[NW + 1];
+#pragma unroll
+                for (int j = 0; j <= NW; j++) v[j] = q[j];
+                uint32_t wd[NW];
+#pragma unroll
+                for (int j = 0; j < NW; j++) wd[j] = __builtin_amdgcn_alignbyte(v[j + 1], v[j], o & 3u);
+#pragma unroll
+                for (int t = 0; t < N; t++) {
+                    auto byte = [&](int k) { return (wd[k >> 2] >> (8 * (k & 3))) & 255u; };
+                    lv[t] = luma3(byte(t * BPP), BPP > 1 ? byte(t * BPP + 1) : 0u,
+                                  BPP > 1 ? byte(t * BPP + 2) : 0u);
+                }
             };
             auto band_rows = [&](int bb, int& r0, int& nrows) {
                 // band bb: output rows [max(A, 0), min(A + SBH, ye - ys)), A = bb SBH - (N - 1);
@@ -1168,7 +1206,12 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
                         double best;
                         bool edge;
                         const int rr = ly - HL - r0;
-                        if constexpr (kOtf) {
+                        if constexpr (kOtf && DCTE_FIX_ALIGNED && SEM == kSemLqr) {
+                            // liblqr: lane l reads window row l (contiguous bytes)
+                            double lv[N];
+                            line_at(rr + l, lx, lv);
+                            refine_group_f<N>([&](int i) { return lv[i]; }, win[grp], l, best, edge);
+                        } else if constexpr (kOtf) {
                             // liblqr: lane l reads window row l; preview: window column l
                             refine_group_f<N>([&](int i) {
                                 return SEM == kSemLqr ? lum_at(rr + l, lx + i) : lum_at(rr + i, lx + l);
