@@ -56,3 +56,17 @@ def test_failing_rank_fails_the_launch():
                        capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode != 0
     assert "needs >=" in r.stderr
+
+
+def test_rank_env_shared_gpu():
+    """--shared-gpu: every rank names its own host to RCCL (NCCL_HOSTID), so
+    ranks that share a device are not refused as duplicates; plain launches
+    leave RCCL's host detection alone."""
+    sys.path.insert(0, ROOT)
+    import bench
+    envs = [bench.rank_env(r, 3, 4242, shared_gpu=True) for r in range(3)]
+    assert len({e["NCCL_HOSTID"] for e in envs}) == 3
+    assert all(e["NCCL_SOCKET_IFNAME"] == "lo" and e["MASTER_ADDR"] == "127.0.0.1" for e in envs)
+    assert [e["RANK"] for e in envs] == ["0", "1", "2"] and envs[0]["WORLD_SIZE"] == "3"
+    plain = bench.rank_env(1, 2, 4242)
+    assert "NCCL_HOSTID" not in plain or plain["NCCL_HOSTID"] == os.environ.get("NCCL_HOSTID")

@@ -23,7 +23,10 @@ def main():
     ap.add_argument("--n", type=int, default=8)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--tile-h", type=int, default=0)
+    ap.add_argument("--lib", default=None, help="libdctenergy_hip.so to load (A/B)")
     a = ap.parse_args()
+    if a.lib:
+        os.environ["DCTE_LIB"] = os.path.abspath(a.lib)
     import torch
     import dctenergy
     from dctenergy import synth
@@ -57,7 +60,7 @@ def main():
             e1.record(s)
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / a.iters
-            print(json.dumps({"pattern": name, "rows": R, "width": W, "n": n, "tile_h": a.tile_h,
+            print(json.dumps({"pattern": name, "lib": os.path.basename(a.lib or "default"), "rows": R, "width": W, "n": n, "tile_h": a.tile_h,
                               "ms_per_step": round(ms, 4), "host_ms_per_step": round(host_ms, 4),
                               "mpx_s": round(R * W / ms / 1e3, 1)}), flush=True)
 
