@@ -7,6 +7,12 @@ ATOL), class flips, the largest relative error, and how many pixels are
 bit-identical.
 
     python tools/full_parity.py [--size 16384] [--size16 8192] [--threads 16]
+                                [--kind natural|lineart|dots|text|grid8] [--n 8,16]
+
+--kind other than natural takes the tie-dense frames of tools/fix_study.py
+(binary line art, isolated dots, 4-px text blocks, 8-px grid: exact edge /
+texture ties decided by the reference's rounding, so most of their flagged
+pixels go through the fp64 refinement), replicated over the channels.
 """
 import argparse
 import json
@@ -25,6 +31,8 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--edges", type=float, default=0.3)
     ap.add_argument("--textures", type=float, default=0.7)
+    ap.add_argument("--kind", default="natural")
+    ap.add_argument("--n", default="2,4,8,16", help="block sizes, comma-separated")
     a = ap.parse_args()
     import torch
     import dctenergy
@@ -36,10 +44,33 @@ def main():
     cases = [(dctenergy.DCTE_LQR, "liblqr", bpp) for bpp in (1, 3)] + \
             [(dctenergy.DCTE_PREVIEW, "preview", bpp) for bpp in (1, 3, 4)]
     with dctenergy.Context(ngpus=1) as ctx:
-        for n in (2, 4, 8, 16):
+        def make(S, bpp):
+            if a.kind == "natural":
+                return synth.natural_rows(0, S, S, bpp, seed=1, device="cuda")
+            g = torch.Generator(device="cuda")
+            g.manual_seed(5)
+            yy = torch.arange(S, device="cuda").view(-1, 1)
+            xx = torch.arange(S, device="cuda").view(1, -1)
+            if a.kind == "lineart":
+                ink = (yy % 23 == 0) | (xx % 31 == 0) | ((xx + 2 * yy) % 97 == 0)
+                grey = torch.where(ink, 0, 255)
+            elif a.kind == "dots":
+                grey = torch.where(torch.rand((S, S), generator=g, device="cuda") < 1 / 64, 255, 16)
+            elif a.kind == "text":
+                blk = torch.rand((S // 4 + 1, S // 4 + 1), generator=g, device="cuda") < 0.3
+                ink = blk.repeat_interleave(4, 0).repeat_interleave(4, 1)[:S, :S]
+                grey = torch.where(ink, 0, 255)
+            elif a.kind == "grid8":
+                grey = torch.where((yy % 8 == 0) | (xx % 8 == 0), 0, 255)
+            else:
+                raise SystemExit(f"unknown --kind {a.kind}")
+            grey = grey.to(torch.uint8)
+            return grey.unsqueeze(-1).expand(S, S, bpp).contiguous()
+
+        for n in [int(v) for v in a.n.split(",")]:
             S = a.size16 if n == 16 else a.size
             for sem, sname, bpp in cases:
-                frame = synth.natural_rows(0, S, S, bpp, seed=1, device="cuda")
+                frame = make(S, bpp)
                 if bpp == 1:
                     frame = frame.reshape(S, S).contiguous()
                 out = torch.empty((S, S), dtype=torch.float32, device="cuda")
@@ -65,7 +96,7 @@ def main():
                         ratio = g[off] / r[off]
                         flips += int((((ratio - lo).abs() < 1e-3 * lo) |
                                       ((ratio - hi).abs() < 1e-3 * hi)).sum())
-                print(json.dumps({"n": n, "semantics": sname, "bpp": bpp, "frame": [S, S],
+                print(json.dumps({"kind": a.kind, "n": n, "semantics": sname, "bpp": bpp, "frame": [S, S],
                                   "edges": e, "textures": t, "pixels": S * S,
                                   "off_tolerance": bad, "class_flips": flips,
                                   "bit_identical": same, "max_rel_err": worst,
