@@ -297,11 +297,6 @@ def main():
         print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         sys.exit(2)
     ndev = torch.cuda.device_count()
-    if world > ndev and args.dist_backend == "nccl" and not args.shared_gpu:
-        print(f"bench: {world} ranks but {ndev} GPU(s): RCCL needs one device per rank "
-              f"(--shared-gpu rehearses RCCL with ranks sharing a device, --dist-backend gloo "
-              f"stages halos through host memory)", file=sys.stderr)
-        sys.exit(2)
     gpu = local % max(1, ndev)          # == local on a full node
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
@@ -499,7 +494,7 @@ def main():
         if world > 1 and not gloo and args.shared_gpu:
             res["config"]["parallelism"] += (" (RCCL rehearsal: distinct NCCL_HOSTID per rank, "
                                              "halos over RCCL's socket transport on loopback)")
-        if world > 1 and ndev < world:
+        if world > 1 and (gloo or args.shared_gpu) and ndev < world:
             res["config"]["parallelism"] += f"; {world} ranks share {ndev} GPU(s)"
         if world == 1 and not args.no_host_path:
             res["host_path"] = host_path(ctx, buf, n, e, t)
