@@ -257,6 +257,37 @@ def test_ties_are_refined_to_reference(ctx):
                 assert ctx.last_refined > 0
 
 
+def _border_dots(H, W, bpp):
+    """Isolated bright pixels on flat ground only at the frame's corners and
+    along its four edges (exact edge / texture ties right at the border):
+    every flagged window is clamped at a frame edge, and the bottom-right ones
+    read the last bytes of the frame."""
+    g = np.full((H, W), 16, np.uint8)
+    for y, x in ((0, 0), (0, W - 1), (H - 1, 0), (H - 1, W - 1), (H - 1, W - 2), (H - 2, W - 1)):
+        g[y, x] = 255
+    g[::7, 0] = g[3::7, 1] = g[::7, W - 1] = g[3::7, W - 2] = 255
+    g[0, ::11] = g[1, 5::11] = g[H - 1, ::11] = g[H - 2, 5::11] = 255
+    return g if bpp == 1 else np.repeat(g[..., None], bpp, -1).copy()
+
+
+@pytest.mark.parametrize("n", [4, 8, 16])
+def test_refinement_at_frame_borders(ctx, n):
+    """Flagged pixels only in windows clamped at the frame borders (odd widths,
+    so the frame's byte count is not a dword multiple): the refinement's
+    per-pixel gathers at the left / right edges and its reads of the frame's
+    last bytes agree with the reference, both semantics, every layer format."""
+    cases = [(dctenergy.DCTE_LQR, bpp) for bpp in (1, 3)] + \
+            [(dctenergy.DCTE_PREVIEW, bpp) for bpp in (1, 3, 4)]
+    for H, W in ((37, 301), (41, 517)):
+        for sem, bpp in cases:
+            img = _border_dots(H, W, bpp)
+            got = ctx.energy_map(img, n, 0.3, 0.7, semantics=sem)
+            refined = ctx.last_refined
+            ref = (O.energy_map if sem == dctenergy.DCTE_LQR else O.preview_map)(img, n, 0.3, 0.7)
+            _assert_tol(got, ref, f"border dots {H}x{W} bpp={bpp} sem={sem} n={n}")
+            assert refined > 0, (H, W, bpp, sem, n)
+
+
 @pytest.mark.parametrize("channels", [1, 3])
 def test_normalize_u8(ctx, channels):
     """energy map -> 8-bit image, both modes, vs numpy restatements."""
