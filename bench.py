@@ -61,6 +61,8 @@ def parse(argv=None):
                     help="after timing, recompute every band from regenerated rows (no "
                          "exchange) and require bit-equality (default on for --gpus > 1)")
     ap.add_argument("--no-check", action="store_true", help="skip that check for --gpus > 1")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="--gpus > 1: skip the end-to-end figure (step + band gather to rank 0)")
     ap.add_argument("--shared-gpu", action="store_true",
                     help="RCCL rehearsal on a box with fewer GPUs than ranks: the self-launched "
                          "ranks get distinct NCCL_HOSTIDs so RCCL accepts several ranks on one "
@@ -283,6 +285,11 @@ def main():
     sys.path.insert(0, os.path.join(ROOT, "dct-carver_amd"))
     if args.cpu_rehearsal:
         sys.exit(cpu_rehearsal(args))
+    # stdout carries exactly the one JSON line: whatever the runtime libraries
+    # print there (RCCL's version banner at communicator init) goes to stderr
+    sys.stdout.flush()
+    result_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
 
@@ -431,6 +438,31 @@ def main():
         if world > 1:
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         check = bool(ok.item())
+        del ref_in, ref_out
+
+    # end to end: the step plus the gather of every band's
+    # map to rank 0 over RCCL, reported beside the kernel-only metric
+    e2e = None
+    if world > 1 and not gloo and not args.no_e2e:
+        reps = 3
+        D.gather_bands(out, band)                     # warm
+        torch.cuda.synchronize()
+        dist.barrier()
+        g0 = time.perf_counter()
+        for _ in range(reps):
+            whole = D.gather_bands(out, band)
+        torch.cuda.synchronize()
+        dist.barrier()
+        gms = torch.tensor([(time.perf_counter() - g0) * 1e3 / reps], dtype=torch.float64, device=dev)
+        dist.all_reduce(gms, op=dist.ReduceOp.MAX)
+        gather_ms = float(gms.item())
+        del whole
+        e2e = {"gather_ms": round(gather_ms, 4),
+               "step_plus_gather_ms": round(ms_per_step + gather_ms, 4),
+               "value": round(total_px / ((ms_per_step + gather_ms) * 1e-3) / 1e6, 1),
+               "unit": "Mpx/s",
+               "what": "one step, then every band's f32 map gathered to rank 0 "
+                       "(dctenergy.dist.gather_bands, RCCL); kernel-only scaling is `value`"}
 
     if rank == 0:
         res = {
@@ -489,6 +521,8 @@ def main():
         }
         if check is not None:
             res["check_bands_bit_exact"] = check
+        if e2e is not None:
+            res["end_to_end"] = e2e
         if world > 1 and gloo:
             res["config"]["parallelism"] += " (halo via gloo rehearsal)"
         if world > 1 and not gloo and args.shared_gpu:
@@ -503,7 +537,7 @@ def main():
             rows = min(rows, H)
             host = buf[:min(H, rows + n)].cpu().numpy()
             res["cpu_baseline"] = cpu_baseline(host, W, n, e, t, rows)
-        print(json.dumps(res), flush=True)
+        print(json.dumps(res), file=result_out, flush=True)
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
