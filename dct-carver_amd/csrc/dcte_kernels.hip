@@ -856,23 +856,22 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
             }
         } else if constexpr (DCTE_FIX_PIPE) {
             // the group (GL = N lanes) takes its strip's entries one at a
-            // time, software-pipelined: entry i + 1's window bytes (and entry
-            // i + 2's list word) are in flight while entry i is transformed.
-            // Lane l fetches image row l of the window as whole dwords (the
-            // row's N pixels: 3 dwords grey, 7 RGB at N = 8) through the
-            // frame's buffer resource; windows clamped at the left / right
-            // frame border, or whose last dword would straddle the end of
-            // the readable bytes, gather per pixel instead (rare).
-            const int l = sl;
-            double* d = win[sgi];
-            constexpr int NW = (N * BPP + 3) / 4;              // dwords of a row's N pixels
-            constexpr int K = NW + 1;                          // loaded: any byte alignment
-            // One fetch buffer: entry i's bytes go to LDS first, then entry
-            // i + 1's loads are issued and fly while entry i is transformed.
+            // time, software-pipelined through ONE fetch buffer: entry i's
+            // bytes go to LDS first, then entry i + 1's loads (and entry
+            // i + 2's list word) are issued and fly while entry i is
+            // transformed.  Lane l fetches image row l of the window as whole
+            // dwords (the row's N pixels: 3 dwords grey, 7 RGB at N = 8)
+            // through the frame's buffer resource; windows clamped at the
+            // left / right frame border, or whose last dword would straddle
+            // the end of the readable bytes, gather per pixel instead (rare).
             // The loads are unconditional (an invalid or per-pixel entry
             // reads past the buffer's end: zeros, no access), so the wait
             // counts are the same on every path; list words are clamped
             // into the strip's own entries.
+            const int l = sl;
+            double* d = win[sgi];
+            constexpr int NW = (N * BPP + 3) / 4;              // dwords of a row's N pixels
+            constexpr int K = NW + 1;                          // loaded: any byte alignment
             uint32_t fv[K];
             uint32_t foff = 0;
             bool fwide = false;
