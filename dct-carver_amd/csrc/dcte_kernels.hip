@@ -66,6 +66,9 @@ namespace dcte {
 #ifndef DCTE_PRIO
 #define DCTE_PRIO 1        // wave priority while staging / converting a group (A/B: -2 % at N = 8 and 16)
 #endif
+#ifndef DCTE_PF2_MAXN
+#define DCTE_PF2_MAXN 4    // N <= this: raw rows prefetched two groups ahead (else one)
+#endif
 #ifndef DCTE_XBAL
 #define DCTE_XBAL 1        // halo-column luma conversions spread one per lane of the last wave
 #endif
@@ -191,8 +194,11 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
             tail |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, (int)(nrec4 + b), 0, 0) << (8u * b);
     }
 
-    uint32_t pref[G][DPT];
-    auto issue = [&](int g) {
+    // raw rows in flight: PFD groups ahead (two register buffers for the
+    // small blocks, whose launches are bound by loads in flight, not VALU)
+    constexpr int PFD = (S == 1 && DCTE_DB && N <= DCTE_PF2_MAXN) ? 2 : 1;
+    uint32_t pref[PFD][G][DPT];
+    auto issue = [&](int g, auto PB) {
 #pragma unroll
         for (int u = 0; u < G; u++) {
             int i = g * G + u;
@@ -200,7 +206,7 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
 #pragma unroll
             for (int q = 0; q < DPT; q++) {
                 const int dw = tx + q * kThreads;
-                pref[u][q] = (dw < NDW) ? __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * dw), 0, 0) : 0u;
+                pref[PB][u][q] = (dw < NDW) ? __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * dw), 0, 0) : 0u;
             }
         }
     };
@@ -245,15 +251,15 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
         }
     };
 
-    // raw dwords of group gg (prefetched in pref) -> raw[b]
-    auto stage = [&](int gg, int b) {
+    // raw dwords of group gg (prefetched in pref[PB]) -> raw[b]
+    auto stage = [&](int gg, int b, auto PB) {
 #pragma unroll
         for (int q = 0; q < DPT; q++) {
             const int dw = tx + q * kThreads;
             if (dw < NDW) {
 #pragma unroll
                 for (int u = 0; u < G; u++) {
-                    uint32_t v = pref[u][q];
+                    uint32_t v = pref[PB][u][q];
                     if (tail_wg) {                 // uniform; a handful of WGs
                         int i = gg * G + u;
                         uint32_t a = (row_start(i < n_in ? i : n_in - 1) & ~3u) + 4u * dw;
@@ -302,7 +308,7 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
         }
     };
     // row pass + column pass for the G rows of group g (luma in lum[b])
-    auto compute = [&](int g, int b) {
+    auto compute = [&](int g, int b) __attribute__((always_inline)) {
         static_for<G>([&](auto U) {
             constexpr int u = decltype(U)::value;
             const int i = g * G + u;
@@ -346,14 +352,45 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
         }
     };
 
-    issue(0);
-    if constexpr (kDB) {
+    constexpr std::integral_constant<int, 0> P0{};
+    issue(0, P0);
+    if constexpr (kDB && PFD == 2) {
+        // As below, with groups g + 2 AND g + 3 in flight while group g is
+        // computed: the group staged next comes from pref[(g + 1) & 1], which
+        // is refilled with group g + 3 right after (loop unrolled by two so
+        // the register buffers are indexed statically).
+        constexpr std::integral_constant<int, 1> P1{};
+        if (ngroups > 1) issue(1, P1);
+        stage(0, 0, P0);
+        if (ngroups > 2) issue(2, P0);
+        __syncthreads();
+        auto step = [&](int g, int b, auto PB) __attribute__((always_inline)) {
+#if DCTE_PRIO
+            __builtin_amdgcn_s_setprio(DCTE_PRIO);
+#endif
+            convert(g, b);
+            if (g + 1 < ngroups) {
+                stage(g + 1, b ^ 1, PB);
+                if (g + 3 < ngroups) issue(g + 3, PB);
+            }
+            __syncthreads();
+#if DCTE_PRIO
+            __builtin_amdgcn_s_setprio(0);
+#endif
+            compute(g, b);
+        };
+        for (int g = 0; g < ngroups; g += 2) {
+            step(g, 0, P1);
+            if (g + 1 >= ngroups) break;
+            step(g + 1, 1, P0);
+        }
+    } else if constexpr (kDB) {
         // One barrier per group: group g is converted and group g + 1 staged
         // before it, group g's passes run after it.  raw[b] / lum[b] are
         // rewritten only after every wave has passed the barrier that follows
         // their last reads (convert(g - 1) / compute(g - 2)).
-        stage(0, 0);
-        if (ngroups > 1) issue(1);
+        stage(0, 0, P0);
+        if (ngroups > 1) issue(1, P0);
         __syncthreads();
         for (int g = 0; g < ngroups; g++) {
             const int b = g & 1;
@@ -362,8 +399,8 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
 #endif
             convert(g, b);
             if (g + 1 < ngroups) {
-                stage(g + 1, b ^ 1);
-                if (g + 2 < ngroups) issue(g + 2);
+                stage(g + 1, b ^ 1, P0);
+                if (g + 2 < ngroups) issue(g + 2, P0);
             }
             __syncthreads();
 #if DCTE_PRIO
@@ -377,8 +414,8 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
 #if DCTE_PRIO
             __builtin_amdgcn_s_setprio(DCTE_PRIO);
 #endif
-            stage(g, 0);
-            if (g + 1 < ngroups) issue(g + 1);
+            stage(g, 0, P0);
+            if (g + 1 < ngroups) issue(g + 1, P0);
             __syncthreads();
             convert(g, 0);
             __syncthreads();
