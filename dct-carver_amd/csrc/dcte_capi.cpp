@@ -50,6 +50,7 @@ struct DpScratch {                 // seam DP (dcte_dp.hip), per stream
 
 struct Device {
     int id = -1;
+    int cus = 0;                   // compute units (queried on first map launch)
     hipStream_t stream = nullptr;  // used by the host entry point
     uint8_t* d_in = nullptr;
     size_t in_cap = 0;
@@ -262,18 +263,24 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     size_t npix = (size_t)(y1 - y0) * (size_t)w;
     if (npix >= (1ULL << 32)) return DCTE_ERANGE;
     // one workgroup's output rows go through one buffer resource
-    // default tile height; a launch that would fill the chip only about once
-    // (a strong-scaling rank's 2048-row band: 1024 workgroups) uses half-height
-    // tiles, whose second round evens out the finish (−3.5 % per band,
-    // tools/band_bench.py, profiles/r02/band_tile_h.jsonl)
     int tile_h = ctx->tile_h > 0 ? ctx->tile_h : dcte::map_default_tile_h(n);
-    if (ctx->tile_h <= 0 && n == 8 &&
-        (long long)dcte::map_tiles_x(n, w) * dcte::map_tiles_y(n, y1 - y0, tile_h) < 2048 &&
-        y1 - y0 >= 1024)
-        tile_h /= 2;
     if ((long long)tile_h * out_stride * 4 >= (1LL << 31)) return DCTE_ERANGE;
 
     DCTE_HIP(ctx, hipSetDevice(d.id));
+    // N = 8 launches of at most two rounds of workgroups (a strong-scaling
+    // rank's 2048- or 4096-row band) step their waves' priority down through
+    // their tiles so the workgroups sharing a CU finish together (see
+    // dcte_map's set_prio): 2048-row band -6 % (vs half-height tiles -2 %),
+    // 4096 -2 %; longer launches even out by themselves (tools/band_bench.py,
+    // profiles/r02/map_fair_ab.jsonl)
+    int fair = 0;
+    if (n == 8) {
+        if (d.cus <= 0 &&
+            hipDeviceGetAttribute(&d.cus, hipDeviceAttributeMultiprocessorCount, d.id) != hipSuccess)
+            d.cus = 256;
+        const long long nwg = (long long)dcte::map_tiles_x(n, w) * dcte::map_tiles_y(n, y1 - y0, tile_h);
+        if (nwg <= 2LL * 4 * d.cus) fair = 3;
+    }
     // refinement lists: one region of 64 * tile_h entries per 64-column strip
     const int tiles_x = dcte::map_tiles_x(n, w), tiles_y = dcte::map_tiles_y(n, y1 - y0, tile_h);
     const size_t ntiles = (size_t)tiles_x * (size_t)tiles_y * (size_t)dcte::map_strips_per_tile(n);
@@ -296,6 +303,7 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     p.y0 = y0;
     p.y1 = y1;
     p.tile_h = tile_h;
+    p.fair = fair;
     p.out = d_out;
     p.out_stride = out_stride;
     p.we = (float)((double)edges / scale);

@@ -20,6 +20,7 @@ struct MapParams {
     int in_row0, in_rows;    // readable input rows (global)
     int y0, y1;              // output rows (global)
     int tile_h;              // output rows per workgroup
+    int fair;                // > 0: priority levels a workgroup steps down through its tile
     float* out;              // row y at out + (y - y0) * out_stride
     long long out_stride;    // floats
     float we, wt;            // edges / textures weights, pre-scaled to luma units

@@ -66,6 +66,9 @@ namespace dcte {
 #ifndef DCTE_PRIO
 #define DCTE_PRIO 1        // wave priority while staging / converting a group (A/B: -2 % at N = 8 and 16)
 #endif
+#ifndef DCTE_TSTAMP
+#define DCTE_TSTAMP 0      // timing-probe builds: per-workgroup timestamps over the output (tools/tstamp.py)
+#endif
 #ifndef DCTE_PF2_MAXN
 #define DCTE_PF2_MAXN 4    // N <= this: raw rows prefetched two groups ahead (else one)
 #endif
@@ -149,6 +152,9 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
     // remap gives each XCD a contiguous run of tiles (strips of a row band in
     // order), so the N - 1 halo columns two neighbouring strips both read
     // come from one L2 instead of being fetched twice.
+#if DCTE_TSTAMP
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     int bx = blockIdx.x, by = blockIdx.y;
     if constexpr (DCTE_XCD) {
         const int nwg = gridDim.x * gridDim.y, L = blockIdx.x + gridDim.x * blockIdx.y;
@@ -352,6 +358,24 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
         }
     };
 
+    // Wave priority.  A wave stages and converts a group at a raised
+    // priority so its workgroup reaches the barrier sooner (DCTE_PRIO).  In
+    // launches of one or two rounds (p.fair > 0, set by the host) the level
+    // also falls as the workgroup gets through its tile: the hardware
+    // otherwise favours the OLDEST waves of a SIMD, so of the workgroups
+    // sharing a CU the first-dispatched finishes long before the last, and
+    // the CU runs the launch's tail below occupancy (tools/tstamp.py, one
+    // round of 128-row tiles: 115-202 us for identical tiles, 137-185 with
+    // the falling level).
+    const int fair = p.fair;                         // uniform
+    auto set_prio = [&](bool staging, int g) __attribute__((always_inline)) {
+        int lvl = staging ? DCTE_PRIO : 0;
+        if (fair > 0) lvl += (fair - 1) - min(fair - 1, g * fair / ngroups);
+        if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
+        else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
+        else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+    };
     constexpr std::integral_constant<int, 0> P0{};
     issue(0, P0);
     if constexpr (kDB && PFD == 2) {
@@ -366,7 +390,7 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
         __syncthreads();
         auto step = [&](int g, int b, auto PB) __attribute__((always_inline)) {
 #if DCTE_PRIO
-            __builtin_amdgcn_s_setprio(DCTE_PRIO);
+            set_prio(true, g);
 #endif
             convert(g, b);
             if (g + 1 < ngroups) {
@@ -375,7 +399,7 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
             }
             __syncthreads();
 #if DCTE_PRIO
-            __builtin_amdgcn_s_setprio(0);
+            set_prio(false, g);
 #endif
             compute(g, b);
         };
@@ -395,7 +419,7 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
         for (int g = 0; g < ngroups; g++) {
             const int b = g & 1;
 #if DCTE_PRIO
-            __builtin_amdgcn_s_setprio(DCTE_PRIO);
+            set_prio(true, g);
 #endif
             convert(g, b);
             if (g + 1 < ngroups) {
@@ -404,7 +428,7 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
             }
             __syncthreads();
 #if DCTE_PRIO
-            __builtin_amdgcn_s_setprio(0);
+            set_prio(false, g);
 #endif
             compute(g, b);
         }
@@ -412,7 +436,7 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
         for (int g = 0; g < ngroups; g++) {
             // stage raw bytes of group g, then prefetch group g + 1
 #if DCTE_PRIO
-            __builtin_amdgcn_s_setprio(DCTE_PRIO);
+            set_prio(true, g);
 #endif
             stage(g, 0, P0);
             if (g + 1 < ngroups) issue(g + 1, P0);
@@ -420,7 +444,7 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
             convert(g, 0);
             __syncthreads();
 #if DCTE_PRIO
-            __builtin_amdgcn_s_setprio(0);
+            set_prio(false, g);
 #endif
             compute(g, 0);
         }
@@ -431,6 +455,18 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
         p.tile_count[st] = nflag[tx];
         p.dirty_list[atomicAdd(p.dirty_count, 1u)] = st;
     }
+#if DCTE_TSTAMP
+    // timing probe builds only (tools/tstamp.py): the workgroup's start /
+    // end on the 100 MHz real-time counter and its hardware slot, written
+    // over the head of the OUTPUT map (the map is wrong in these builds)
+    if (tx == 0) {
+        const unsigned L = blockIdx.x + gridDim.x * blockIdx.y;
+        unsigned long long* ts = reinterpret_cast<unsigned long long*>(p.out);
+        ts[3 * L] = t_start;
+        ts[3 * L + 1] = __builtin_amdgcn_s_memrealtime();
+        ts[3 * L + 2] = (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+    }
+#endif
 }
 
 // ------------------------------------------------------------------ refinement
