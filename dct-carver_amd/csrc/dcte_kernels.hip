@@ -367,7 +367,7 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
     // the CU runs the launch's tail below occupancy (tools/tstamp.py, one
     // round of 128-row tiles: 115-202 us for identical tiles, 137-185 with
     // the falling level).
-    const int fair = p.fair;                         // uniform
+    const int fair = N == 8 ? p.fair : 0;            // uniform; the host sets it for N = 8 only
     auto set_prio = [&](bool staging, int g) __attribute__((always_inline)) {
         int lvl = staging ? DCTE_PRIO : 0;
         if (fair > 0) lvl += (fair - 1) - min(fair - 1, g * fair / ngroups);
