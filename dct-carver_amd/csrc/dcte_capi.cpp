@@ -270,9 +270,10 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     // N = 8 launches of at most two rounds of workgroups (a strong-scaling
     // rank's 2048- or 4096-row band) step their waves' priority down through
     // their tiles so the workgroups sharing a CU finish together (see
-    // dcte_map's set_prio): 2048-row band -6 % (vs half-height tiles -2 %),
-    // 4096 -2 %; longer launches even out by themselves (tools/band_bench.py,
-    // profiles/r02/map_fair_ab.jsonl)
+    // dcte_map's set_prio): 2048-row band -6 % against the same tiles
+    // without it and -1..-2 % against the half-height tiles used before,
+    // 4096 rows -2.5 %; longer launches even out by themselves
+    // (tools/band_bench.py, profiles/r02/map_fair_ab.jsonl)
     int fair = 0;
     if (n == 8) {
         if (d.cus <= 0 &&
