@@ -239,6 +239,30 @@ def test_stress_frames_full(ctx, n):
         print(name, n, "refined", refined, st)
 
 
+def test_tie_dense_full_size(ctx):
+    """The worst realistic inputs for the fp64 refinement at the metric's
+    size (16384^2, N=8, e=0.3 t=0.7): line art as RGB (2.7 % of the pixels
+    flagged, most strips dense) and dots on flat ground (0.37 %, sparse
+    strips) -- every pixel against the oracle, 0 class flips."""
+    torch = _torch()
+    S = 16384
+    yy, xx = np.ogrid[0:S, 0:S]
+    ink = (yy % 23 == 0) | (xx % 31 == 0) | ((xx + 2 * yy) % 97 == 0)
+    line = np.repeat(np.where(ink, 0, 255).astype(np.uint8)[..., None], 3, -1)
+    del ink
+    dots = np.where(np.random.default_rng(21).random((S, S), dtype=np.float32) < 1 / 64,
+                    255, 16).astype(np.uint8)
+    for name, img in (("lineart_rgb", line), ("dots_grey", dots)):
+        out = torch.from_numpy(ctx.energy_map(img, 8, 0.3, 0.7)).cuda()
+        refined = ctx.last_refined
+        ref = O.energy_map(img, 8, 0.3, 0.7, nthreads=NTHREADS)
+        st = _compare_full(out, ref, 0.3, 0.7, f"{name} {S}^2 N=8")
+        print(name, "refined", refined, st)
+        assert refined > 100000
+        del out, ref
+        torch.cuda.empty_cache()
+
+
 def test_ties_are_refined_to_reference(ctx):
     """Images full of exact edge/texture ties (isolated pixels on flat ground)
     match the reference bit-exactly where the class is decided by rounding."""
