@@ -20,10 +20,12 @@
 #include "dcte_kernels.h"
 #include "dcte_luma.h"
 #include "dcte_norm.h"
+#include "dcte_ref64.h"
 
 namespace {
 
 constexpr double kDefaultTieTau = 4e-6;
+constexpr int kMaxGridY = 65535;   // launch grid limit in y (map tiles of a band)
 
 struct FixScratch {
     // [0] list length (points / seam), [1] refined, [2 + phase] dirty strips of
@@ -110,6 +112,7 @@ struct dcte_ctx {
     int tile_h = 0;                 // DCTE_OPT_TILE_H (0: the kernel's default)
     bool dp_bandwise = false;       // DCTE_OPT_DP_BANDWISE
     unsigned dp_spin_limit = 0;     // DCTE_OPT_DP_SPIN_LIMIT (0: the kernel's default)
+    unsigned long long* stamps = nullptr;   // DCTE_OPT_TSTAMP_BUF (timing-probe builds)
     std::vector<ProfEvent> prof;
     long long last_refined = 0;
     std::string last_error;
@@ -262,9 +265,16 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     if (span >= (1LL << 32)) return DCTE_ERANGE;
     size_t npix = (size_t)(y1 - y0) * (size_t)w;
     if (npix >= (1ULL << 32)) return DCTE_ERANGE;
-    // one workgroup's output rows go through one buffer resource
+    // one workgroup's output rows go through one buffer resource; a band
+    // shorter than a tile is one tile of exactly its rows (same results, and
+    // the refinement list below is sized for the rows that exist)
     int tile_h = ctx->tile_h > 0 ? ctx->tile_h : dcte::map_default_tile_h(n);
+    if (tile_h > y1 - y0) tile_h = y1 - y0;
     if ((long long)tile_h * out_stride * 4 >= (1LL << 31)) return DCTE_ERANGE;
+    if (dcte::map_tiles_y(n, y1 - y0, tile_h) > kMaxGridY) {
+        ctx->last_error = "tile rows exceed the launch grid (raise DCTE_OPT_TILE_H)";
+        return DCTE_ERANGE;
+    }
 
     DCTE_HIP(ctx, hipSetDevice(d.id));
     // N = 8 launches of at most two rounds of workgroups (a strong-scaling
@@ -317,6 +327,7 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     p.dirty_list = f->d_tiles + ntiles;
     p.dirty_count = f->d_count + 2 + f->phase;
     p.dirty_next = f->d_count + 2 + (f->phase ^ 1u);
+    p.stamps = ctx->stamps;
 
     dcte::TileFixParams q{};
     q.m = p;
@@ -324,20 +335,32 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     q.fix_total = f->d_count + 1;
     q.tiles_x = tiles_x;
 
-    f->phase ^= 1u;                 // the next launch on this stream uses the other counter
+    // Any failure from here on leaves both dirty counters zeroed on the
+    // stream: a map launch that never ran did not zero its successor's counter,
+    // and a later call must not walk an older launch's dirty list.
+    auto fail = [&](hipError_t e, const char* where) {
+        (void)hipMemsetAsync(f->d_count + 2, 0, 2 * sizeof(unsigned), s);
+        return hip_fail(ctx, e, where);
+    };
+    hipError_t e = hipSuccess;
     if (ctx->profile) {
         ProfEvent ev{d.id, nullptr, nullptr};
-        DCTE_HIP(ctx, hipEventCreate(&ev.a));
-        DCTE_HIP(ctx, hipEventCreate(&ev.b));
-        DCTE_HIP(ctx, hipEventRecord(ev.a, s));
-        DCTE_HIP(ctx, dcte::launch_map(n, bpp, sem, p, s));
-        DCTE_HIP(ctx, hipEventRecord(ev.b, s));
-        ctx->prof.push_back(ev);
-    } else {
-        DCTE_HIP(ctx, dcte::launch_map(n, bpp, sem, p, s));
+        if ((e = hipEventCreate(&ev.a)) != hipSuccess) return fail(e, "hipEventCreate");
+        if ((e = hipEventCreate(&ev.b)) != hipSuccess) {
+            (void)hipEventDestroy(ev.a);
+            return fail(e, "hipEventCreate");
+        }
+        ctx->prof.push_back(ev);      // dcte_profile_read destroys them
+        if ((e = hipEventRecord(ev.a, s)) != hipSuccess) return fail(e, "hipEventRecord");
+        if ((e = dcte::launch_map(n, bpp, sem, p, s)) != hipSuccess) return fail(e, "launch_map");
+        if ((e = hipEventRecord(ev.b, s)) != hipSuccess) return fail(e, "hipEventRecord");
+    } else if ((e = dcte::launch_map(n, bpp, sem, p, s)) != hipSuccess) {
+        return fail(e, "launch_map");
     }
-    if ((p.we != p.wt && ctx->tie_tau > 0) || ctx->tie_tau >= 1.0)
-        DCTE_HIP(ctx, dcte::launch_fix_tiles(n, bpp, sem, q, s));
+    f->phase ^= 1u;   // the launch ran: the next one uses the counter it zeroed
+    if ((p.we != p.wt && ctx->tie_tau > 0) || ctx->tie_tau >= 1.0) {
+        if ((e = dcte::launch_fix_tiles(n, bpp, sem, q, s)) != hipSuccess) return fail(e, "launch_fix_tiles");
+    }
     return DCTE_OK;
 }
 
@@ -628,6 +651,11 @@ int dcte_set_option(dcte_ctx* ctx, int option, double value)
         // band-wise launches
         for (Device& d : ctx->devs)
             for (auto& kv : d.dp) kv.second.max_tiles = -1;
+        return DCTE_OK;
+    case DCTE_OPT_TSTAMP_BUF:
+        // a device address (exact in a double below 2^53); 0 = none
+        if (!(value >= 0 && value < 9007199254740992.0)) return DCTE_EINVAL;
+        ctx->stamps = reinterpret_cast<unsigned long long*>((uintptr_t)value);
         return DCTE_OK;
     default: return DCTE_EINVAL;
     }
@@ -1003,6 +1031,27 @@ int dcte_carve(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t r
         drain(ctx, 1);
         return rc;
     }
+    // the seams first: a search that timed out is re-run from the caller's px
+    // before anything is written to out (which may overlap px)
+    std::vector<int> own;
+    int* hs = seam_cols;
+    if (seams > 0 && !hs) {
+        own.resize((size_t)seams * H);
+        hs = own.data();
+    }
+    if (seams > 0) {
+        DCTE_HIP(ctx, hipMemcpyAsync(hs, d_seams, sizeof(int) * (size_t)seams * H,
+                                     hipMemcpyDeviceToHost, s));
+        DCTE_HIP(ctx, hipStreamSynchronize(s));
+    }
+    for (int k = 0; k < seams; k++)
+        if (hs[(size_t)k * H] < 0) {
+            if (dp_fall_back(d, s))   // out is untouched: carve again band-wise
+                return dcte_carve(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics,
+                                  seams, transposed, out, seam_cols);
+            ctx->last_error = "seam search timed out waiting for a neighbour tile";
+            return DCTE_EHIP;
+        }
     const int Wo = W - seams;
     if (transposed) {   // H x Wo carved frame -> Wo x H = (h - seams) x w
         DCTE_HIP(ctx, dcte::launch_transpose_u8(d_px, (long long)pitch, H, Wo, bpp, d_tmp,
@@ -1013,26 +1062,7 @@ int dcte_carve(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t r
         DCTE_HIP(ctx, hipMemcpy2DAsync(out, (size_t)Wo * bpp, d_px, pitch, (size_t)Wo * bpp, H,
                                        hipMemcpyDeviceToHost, s));
     }
-    std::vector<int> own;
-    int* hs = seam_cols;
-    if (seams > 0 && !hs) {
-        own.resize((size_t)seams * H);
-        hs = own.data();
-    }
-    if (seams > 0)
-        DCTE_HIP(ctx, hipMemcpyAsync(hs, d_seams, sizeof(int) * (size_t)seams * H,
-                                     hipMemcpyDeviceToHost, s));
-    rc = sync_bands(ctx, 1);
-    if (rc) return rc;
-    for (int k = 0; k < seams; k++)
-        if (hs[(size_t)k * H] < 0) {
-            if (dp_fall_back(d, s))   // the input is still on the host: carve again
-                return dcte_carve(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics,
-                                  seams, transposed, out, seam_cols);
-            ctx->last_error = "seam search timed out waiting for a neighbour tile";
-            return DCTE_EHIP;
-        }
-    return DCTE_OK;
+    return sync_bands(ctx, 1);
 }
 
 int dcte_energy_map(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride,
@@ -1187,6 +1217,42 @@ int dcte_profile_read(dcte_ctx* ctx, long long* launches, double* kernel_ms)
     *kernel_ms = total;
     ctx->prof.clear();
     return rc;
+}
+
+// ---- context-free CPU entries --------------------------------
+// The per-window callback body for a caller that keeps its own reading
+// windows on the CPU (a carver after seams shrank it): dctNxN
+// (src/dct.c:77-94) + weighted_max_dct_correlation (src/dct.c:96-110) in
+// fp64 in the reference's operation order (dcte_ref64.h, the same functions
+// the device refinement runs).  No device, no context, no fallback role:
+// the GPU entry points never call these.
+int dcte_energy_window(int n, const double* win, float edges, float textures, float* out)
+{
+    if (!valid_n(n) || !win || !out) return DCTE_EINVAL;
+    double d[16 * 16];
+    memcpy(d, win, sizeof(double) * (size_t)n * (size_t)n);
+    double ct[4];
+    small_twiddles(n, ct);
+    dcte::r64::transform(n, d, ct);
+    *out = dcte::r64::weighted_max(n, d, edges, textures);
+    return DCTE_OK;
+}
+
+int dcte_normalize_u8_host(const float* E, size_t n, int mode, int channels, uint8_t* out)
+{
+    if (!E || !out || n == 0 || !valid_norm(mode, channels)) return DCTE_EINVAL;
+    unsigned kmin = 0xffffffffu, kmax = 0u;
+    for (size_t i = 0; i < n; i++) {
+        const unsigned k = dcte::norm_fkey(E[i]);
+        kmin = k < kmin ? k : kmin;
+        kmax = k > kmax ? k : kmax;
+    }
+    const float mn = dcte::norm_funkey(kmin), mx = dcte::norm_funkey(kmax);
+    for (size_t i = 0; i < n; i++) {
+        const uint8_t v = dcte::norm_one(E[i], mn, mx, mode);
+        for (int c = 0; c < channels; c++) out[i * (size_t)channels + c] = v;
+    }
+    return DCTE_OK;
 }
 
 long long dcte_last_refined(const dcte_ctx* ctx) { return ctx ? ctx->last_refined : 0; }

@@ -36,6 +36,9 @@ struct MapParams {
     unsigned* dirty_list;
     unsigned* dirty_count;   // zero when the launch starts
     unsigned* dirty_next;    // zeroed by this launch: the next launch's dirty_count
+    // timing-probe builds only (DCTE_TSTAMP): 3 words per workgroup {start,
+    // end, HW_ID}, a buffer nothing else reads (null: no stamps)
+    unsigned long long* stamps;
 };
 
 // dcte_fix_strips: the map launch's own parameters plus the fp64 pieces

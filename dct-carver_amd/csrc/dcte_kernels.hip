@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <utility>
 
 #include "dcte_kernels.h"
@@ -457,11 +458,11 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
     }
 #if DCTE_TSTAMP
     // timing probe builds only (tools/tstamp.py): the workgroup's start /
-    // end on the 100 MHz real-time counter and its hardware slot, written
-    // over the head of the OUTPUT map (the map is wrong in these builds)
-    if (tx == 0) {
+    // end on the 100 MHz real-time counter and its hardware slot, into a
+    // buffer of their own (the map itself stays right)
+    if (tx == 0 && p.stamps) {
         const unsigned L = blockIdx.x + gridDim.x * blockIdx.y;
-        unsigned long long* ts = reinterpret_cast<unsigned long long*>(p.out);
+        unsigned long long* ts = p.stamps;
         ts[3 * L] = t_start;
         ts[3 * L + 1] = __builtin_amdgcn_s_memrealtime();
         ts[3 * L + 2] = (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
@@ -1407,6 +1408,8 @@ static void launch_fix_n(const FixParams& p, hipStream_t s)
         hipLaunchKernelGGL((dcte_fix<N, kSemPreview>), dim3(blocks), dim3(kFixThreads), 0, s, p);
 }
 
+constexpr int kMaxDevices = 64;
+
 template <int N, int BPP, int SEM>
 static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
 {
@@ -1414,17 +1417,22 @@ static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
         return hipErrorInvalidValue;
     const int nstrips = p.tiles_x * FixStrip<N, SEM>::SPT * ((p.m.y1 - p.m.y0 + p.m.tile_h - 1) / p.m.tile_h);
     // one wave per block, as many as the device holds at once (LDS-bound:
-    // ~10 per CU at N = 8 RGB); each walks the dirty list in strip batches
-    static int resident = 0;
+    // ~10 per CU at N = 8 RGB); each walks the dirty list in strip batches.
+    // Cached per device (CU counts may differ between devices).
+    static std::atomic<int> cache[kMaxDevices];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    int resident = dev >= 0 && dev < kMaxDevices ? cache[dev].load(std::memory_order_relaxed) : 0;
     if (!resident) {
-        int dev = 0, cus = 0, per_cu = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
+        int cus = 0, per_cu = 0;
+        if (dev >= 0 &&
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
             hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dcte_fix_strips<N, BPP, SEM>, 64, 0) ==
                 hipSuccess && cus > 0 && per_cu > 0)
             resident = cus * per_cu;
         else
             resident = 2048;
+        if (dev >= 0 && dev < kMaxDevices) cache[dev].store(resident, std::memory_order_relaxed);
     }
     const int blocks = nstrips < resident ? nstrips : resident;
     hipLaunchKernelGGL((dcte_fix_strips<N, BPP, SEM>), dim3(blocks), dim3(64), 0, s, p);

@@ -22,16 +22,8 @@
 
 namespace dcte {
 
-// order-preserving float <-> uint key (total order on non-NaN floats)
-__device__ __forceinline__ unsigned fkey(float f)
-{
-    unsigned b = __float_as_uint(f);
-    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-}
-__device__ __forceinline__ float funkey(unsigned k)
-{
-    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
-}
+__device__ __forceinline__ unsigned fkey(float f) { return norm_fkey(f); }
+__device__ __forceinline__ float funkey(unsigned k) { return norm_funkey(k); }
 
 // keys[0] = min key, keys[1] = max key; caller initialises to (~0u, 0u)
 __global__ __launch_bounds__(256) void dcte_minmax(const float* __restrict__ e, long long n,
@@ -78,17 +70,6 @@ __global__ void dcte_keys_to_floats(const unsigned* keys, float* minmax)
 {
     minmax[0] = funkey(keys[0]);
     minmax[1] = funkey(keys[1]);
-}
-
-__device__ __forceinline__ uint8_t norm_one(float d, float mn, float mx, int mode)
-{
-    if (!(mx > mn)) return 0;
-    if (mode == kNormPreview) {
-        double v = 255.0 * (((double)d - (double)mn) / ((double)mx - (double)mn));
-        return (uint8_t)(int)(v + 0.5);
-    }
-    float v = (d - mn) / (mx - mn);
-    return (uint8_t)(int)(v * 255.0f);
 }
 
 __global__ __launch_bounds__(256) void dcte_to_u8(const float* __restrict__ e, long long n,

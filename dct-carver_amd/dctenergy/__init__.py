@@ -35,6 +35,7 @@ DCTE_OPT_PIN_HOST = 3
 DCTE_OPT_TILE_H = 4
 DCTE_OPT_DP_BANDWISE = 5
 DCTE_OPT_DP_SPIN_LIMIT = 6
+DCTE_OPT_TSTAMP_BUF = 7
 DCTE_NORM_LQR = 0
 DCTE_NORM_PREVIEW = 1
 DCTE_CREATE_SAME_DEVICE = 1
@@ -46,7 +47,8 @@ EXPORTS = ("dcte_abi_version", "dcte_device_count", "dcte_create", "dcte_destroy
            "dcte_last_error", "dcte_normalize_u8", "dcte_energy_image_u8", "dcte_minmax_device",
            "dcte_normalize_u8_device", "dcte_seam_carve_device", "dcte_energy_points",
            "dcte_energy_points_device", "dcte_seam_find_device", "dcte_seam_find",
-           "dcte_carve", "dcte_energy_windows", "dcte_energy_windows_device")
+           "dcte_carve", "dcte_energy_windows", "dcte_energy_windows_device",
+           "dcte_energy_window", "dcte_normalize_u8_host")
 
 _lib = None
 
@@ -144,6 +146,10 @@ def lib():
     L.dcte_seam_find.argtypes = [vp, vp, i, i, vp]
     L.dcte_carve.restype = i
     L.dcte_carve.argtypes = [vp, vp, i, i, i, ctypes.c_size_t, i, f, f, i, i, i, vp, vp]
+    L.dcte_energy_window.restype = i
+    L.dcte_energy_window.argtypes = [i, vp, f, f, vp]
+    L.dcte_normalize_u8_host.restype = i
+    L.dcte_normalize_u8_host.argtypes = [vp, ctypes.c_size_t, i, i, vp]
     L.dcte_strerror.restype = ctypes.c_char_p
     L.dcte_strerror.argtypes = [ctypes.c_int]
     L.dcte_last_error.restype = ctypes.c_char_p
@@ -154,6 +160,32 @@ def lib():
 
 def device_count():
     return lib().dcte_device_count()
+
+
+# -- context-free CPU entries: no device, no context
+def energy_window(win, edges=0.5, textures=0.5):
+    """One N x N float64 window in the reference's data[i][j] layout (i = x
+    offset) -> weighted_max_dct_correlation(dctNxN(window)) as float32
+    (src/dct.c:77-110), computed on the CPU in the reference's fp64 order."""
+    win = np.ascontiguousarray(win, dtype=np.float64)
+    if win.ndim != 2 or win.shape[0] != win.shape[1]:
+        raise ValueError("win must be N x N")
+    out = ctypes.c_float()
+    rc = lib().dcte_energy_window(win.shape[0], win.ctypes.data, edges, textures,
+                                  ctypes.byref(out))
+    if rc != DCTE_OK:
+        raise DcteError(rc)
+    return np.float32(out.value)
+
+
+def normalize_u8_host(E, mode=DCTE_NORM_PREVIEW, channels=1):
+    """Energy map -> u8 layer on the CPU (the bytes dcte_normalize_u8 gives)."""
+    E = np.ascontiguousarray(E, dtype=np.float32)
+    out = np.empty(E.shape + ((channels,) if channels > 1 else ()), np.uint8)
+    rc = lib().dcte_normalize_u8_host(E.ctypes.data, E.size, mode, channels, out.ctypes.data)
+    if rc != DCTE_OK:
+        raise DcteError(rc)
+    return out
 
 
 class Context:
@@ -430,5 +462,6 @@ class Context:
 
 
 __all__ = ["Context", "DcteError", "lib", "device_count", "LIB_PATH", "EXPORTS",
+           "energy_window", "normalize_u8_host",
            "DCTE_LQR", "DCTE_PREVIEW", "DCTE_OPT_TIE_TAU", "DCTE_OPT_PROFILE", "DCTE_OPT_PIN_HOST", "DCTE_OPT_TILE_H", "DCTE_OPT_DP_BANDWISE", "DCTE_OPT_DP_SPIN_LIMIT",
            "DCTE_NORM_LQR", "DCTE_NORM_PREVIEW"]

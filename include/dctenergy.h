@@ -92,6 +92,10 @@ extern "C" {
                                again band-wise and keep that stream band-wise.
                                Setting this option re-enables the single
                                launch. */
+#define DCTE_OPT_TSTAMP_BUF 7 /* diagnostic, timing-probe builds (DCTE_TSTAMP=1)
+                               only: device address of a buffer of 3 uint64
+                               per map workgroup {start, end, HW_ID}; 0 = none.
+                               Product builds ignore it. */
 
 typedef struct dcte_ctx dcte_ctx;
 
@@ -250,6 +254,21 @@ int dcte_carve(dcte_ctx *ctx, const uint8_t *px, int w, int h, int bpp, size_t r
 /* host buffers: E (n floats) -> out (n*channels bytes), on the first device */
 int dcte_normalize_u8(dcte_ctx *ctx, const float *E, size_t n, int mode, int channels,
                       uint8_t *out);
+
+/* ---- context-free CPU entries -------------------------------
+ * No context and no device: plain host code, for a caller that keeps its own
+ * reading windows on the CPU (liblqr's per-pixel callback after seams shrank
+ * the carver, src/render.c:134-157,377).  The GPU entry points never fall
+ * back to these.
+ *
+ * dcte_energy_window: one window of n*n doubles in the reference's data[i][j]
+ *   layout (src/render.c:146-152: i = x offset, j = y offset, luma in
+ *   [0, 1]) -> *out = weighted_max_dct_correlation(dctNxN(window))
+ *   (src/dct.c:77-110) in fp64 in the reference's operation order:
+ *   bit-identical to the reference.  The window is not modified.
+ * dcte_normalize_u8_host: dcte_normalize_u8 without a device (same bytes). */
+int dcte_energy_window(int n, const double *win, float edges, float textures, float *out);
+int dcte_normalize_u8_host(const float *E, size_t n, int mode, int channels, uint8_t *out);
 
 /* energy map + normalisation without the f32 round trip to the host: out is
  * w*h*channels bytes.  Several devices: band maps, one global min/max. */

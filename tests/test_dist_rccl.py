@@ -51,3 +51,35 @@ def test_bands_over_rccl(world, H, W, n):
     assert res["halo_exact"], "halo rows received over RCCL differ from the global frame"
     assert res["map_bit_exact"], "gathered band maps differ from the single-device map"
     assert res["u8_bit_exact"], "band-normalised u8 layer differs from the single-device layer"
+
+
+@pytest.mark.gpu
+def test_config4_bench_eight_ranks_on_one_gpu():
+    """BASELINE configs[3] as the driver's scaling run executes it, rehearsed
+    on one GPU: bench.py --gpus 8 self-launches 8 RCCL ranks (one 16384^2 RGB
+    frame, 2048-row bands, halos over RCCL point-to-point; distinct
+    NCCL_HOSTIDs so RCCL accepts 8 ranks on one device), times 3 steps, then
+    re-maps every band from regenerated rows without any exchange and
+    requires bit-equality (check_bands_bit_exact), and gathers the bands to
+    rank 0 (end_to_end).  Basis: the band halo of src/render.c:146-152."""
+    import signal
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--shared-gpu",
+           "--steps", "3", "--warmup", "1"]
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=150)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)      # the rank processes too
+        p.communicate()
+        raise
+    assert p.returncode == 0, err[-3000:]
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    res = json.loads(lines[0])
+    print(json.dumps(res))
+    assert res["n_gpus"] == 8 and res["scaling"] == "strong"
+    assert res["config"]["global_frame"] == [16384, 16384] and res["config"]["rows_per_gpu"] == 2048
+    assert res["check_bands_bit_exact"] is True
+    assert res["end_to_end"]["gather_ms"] > 0
+    assert res["value"] > 0 and res["roofline"]["launches_timed"] > 0

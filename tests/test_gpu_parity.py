@@ -487,3 +487,29 @@ def test_refine_all_bit_exact_every_layout(n):
                     assert c.last_refined == img.shape[0] * img.shape[1]
                 got = c.energy_map(img, n, 0.3, 0.7, semantics=dctenergy.DCTE_PREVIEW)
                 assert np.array_equal(got, O.preview_map(img, n, 0.3, 0.7)), (n, th, img.shape, "preview")
+
+
+def test_failed_call_then_good_call(ctx):
+    """A call the library rejects after the refinement scratch of its stream
+    exists (tile rows past the launch grid's y limit -> DCTE_ERANGE) leaves
+    nothing behind: the next calls on the same stream refine exactly the
+    pixels the fp32 path flags, and match the reference (a stale
+    dirty-strip counter would walk an older launch's list)."""
+    rng = np.random.default_rng(17)
+    img = (rng.random((96, 160)) < 0.03).astype(np.uint8) * 255
+    ref = O.energy_map(img, 8, 0.3, 0.7)
+    _, me, mt = EM.energy_map(img, 8, 0.3, 0.7)
+    flagged = int(EM.refine_mask(me, mt, 0.3, 0.7).sum())
+    assert flagged > 0
+    _assert_tol(ctx.energy_map(img, 8, 0.3, 0.7), ref, "before")
+    tall = np.zeros((70000, 2), np.uint8)
+    try:
+        ctx.set_option(dctenergy.DCTE_OPT_TILE_H, 1)
+        with pytest.raises(dctenergy.DcteError) as e:
+            ctx.energy_map(tall, 8, 0.3, 0.7)
+        assert e.value.code == dctenergy.DCTE_ERANGE
+    finally:
+        ctx.set_option(dctenergy.DCTE_OPT_TILE_H, 0)
+    for _ in range(2):
+        _assert_tol(ctx.energy_map(img, 8, 0.3, 0.7), ref, "after")
+        assert ctx.last_refined == flagged

@@ -4,7 +4,8 @@
     python tools/tstamp.py --lib dct-carver_amd/build/variants/tstamp.so --rows 2048 [--tile-h 128]
 
 The probe build writes each workgroup's start / end on the 100 MHz real-time
-counter and its HW_ID over the head of the output map; this prints, for a
+counter and its HW_ID into a stamp buffer of its own (DCTE_OPT_TSTAMP_BUF;
+the map stays right); this prints, for a
 band of --rows rows of a 16384-wide RGB frame (N = 8): the spread of start
 times (dispatch ramp), the workgroup durations, the spread of end times
 (tail), and the same split by co-residency slot on a CU.  One JSON line.
@@ -38,16 +39,20 @@ def main():
     buf = synth.natural_rows(Y0 - hl, R + hl + hr, W, 3, seed=0, device="cuda")
     out = torch.empty((R, W), dtype=torch.float32, device="cuda")
     s = torch.cuda.current_stream()
+    tw = 256 if n != 16 else 64
+    nwg = ((W + tw - 1) // tw) * ((R + a.tile_h - 1) // a.tile_h)
+    stamps = torch.zeros(3 * nwg, dtype=torch.int64, device="cuda")
     with dctenergy.Context(ngpus=1) as ctx:
         ctx.set_option(dctenergy.DCTE_OPT_TILE_H, a.tile_h)
+        ctx.set_option(dctenergy.DCTE_OPT_TSTAMP_BUF, stamps.data_ptr())
         ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, 0.0)     # the map launch alone
         for _ in range(6):
             ctx.energy_map_device(buf.data_ptr(), buf.stride(0), W, H, 3, Y0 - hl, buf.shape[0],
                                   Y0, Y0 + R, n, 0.3, 0.7, out.data_ptr(), out.stride(0), s.cuda_stream)
         torch.cuda.synchronize()
-    tw = 256 if n != 16 else 64
-    nwg = ((W + tw - 1) // tw) * ((R + a.tile_h - 1) // a.tile_h)
-    ts = out.flatten()[:6 * nwg].cpu().numpy().view(np.uint64).reshape(nwg, 3).astype(np.int64)
+    ts = stamps.cpu().numpy().reshape(nwg, 3)
+    if not ts[:, 1].any():
+        raise SystemExit("no stamps written: --lib is not a DCTE_TSTAMP=1 build")
     start, end, hwid = ts[:, 0], ts[:, 1], ts[:, 2]
     t0 = start.min()
     us = lambda v: round(float(v) / 100.0, 2)        # 100 MHz ticks -> us
