@@ -219,6 +219,8 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
     };
 
     float ring[N][CH];
+    // matrix-pipe operands of the N = 8 texture columns (every lane active here)
+    const Mfma8K mk8 = (N == 8 && DCTE_MFMA8 > 0) ? mfma8_consts() : Mfma8K{};
     const float we = p.we, wt = p.wt;
     // output rows [ys, ye) of this workgroup through one buffer resource
     const int ostride4 = (int)(p.out_stride * 4);
@@ -333,7 +335,10 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
                 }
                 if (i >= N - 1) {
                     float mt, me;
-                    Cols<N>::template run<(u + 1) % N>(ring, lane_p, mt, me);
+                    if constexpr (N == 8 && DCTE_MFMA8 > 0)
+                        Cols<N>::template run<(u + 1) % N, true>(ring, lane_p, mt, me, mk8);
+                    else
+                        Cols<N>::template run<(u + 1) % N>(ring, lane_p, mt, me);
                     if constexpr (S == 4) {
                         part_t[u][lane_p][c] = mt;
                         if ((lane_p & 1) == 0) part_e[u][lane_p >> 1][c] = me;

@@ -32,7 +32,130 @@
 #define DCTE_PQ2 1   // N = 8: fold |X1|, |X7| through their own chain (dct8_col_parts)
 #endif
 
+#ifndef DCTE_MFMA8
+#define DCTE_MFMA8 0     // N = 8: texture columns k1 = 8 - DCTE_MFMA8 .. 7 on the matrix pipe (0..6)
+#endif
+#ifndef DCTE_MFMA8_SYM
+#define DCTE_MFMA8_SYM 1 // 1: the VALU forms x_t +- x_{7-t}, 2 x 4 MFMAs per column; 0: 2 x 8 MFMAs on x
+#endif
+
 namespace dcte {
+
+// ------------------------------------------------------------------ matrix pipe
+// A texture column of the N = 8 second pass on the matrix pipe, co-issued with
+// the VALU columns.  v_mfma_f32_4x4x1_16b_f32 is 16 independent 4x4 outer
+// products per wave: D[r] of lane l += A(lane 4 (l / 4) + r) * B(lane l) --
+// with B = the lane's own ring value and A = a per-lane constant (lane l holds
+// row l & 3 of the transform matrix) every lane accumulates four outputs of
+// ITS OWN column, one fmaf per output per instruction (the MFMA is bit-for-bit
+// an fmaf chain in program order).  The host side evaluates the same chains
+// with fmaf, so tests/emu stays bit-identical to the device.
+// Hat units as dct8: X[0] = sum x_j, X[k] = sqrt2 sum x_j cos(pi (2j+1) k / 16).
+//   kMe[r][t]: X[2r] from s_t = x_t + x_{7-t};  kMo[r][t]: X[2r+1] from d_t = x_t - x_{7-t}
+constexpr float kMe[4][4] = {{1.0f, 1.0f, 1.0f, 1.0f},
+                             {k8E, k8F, -k8F, -k8E},
+                             {1.0f, -1.0f, -1.0f, 1.0f},
+                             {k8F, -k8E, k8E, -k8F}};
+constexpr float kMo[4][4] = {{k8A, k8B, k8C, k8D},
+                             {k8B, -k8D, -k8A, -k8C},
+                             {k8C, -k8A, k8D, k8B},
+                             {k8D, -k8C, k8B, -k8A}};
+
+struct Mfma8K {
+    float e[4], o[4];    // device: this lane's A operands (row lane & 3); unused on the host
+};
+
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef float dcte_v4f __attribute__((ext_vector_type(4)));
+#endif
+#if defined(__HIPCC__)
+// this lane's A operands, made opaque so they stay in 8 registers for the
+// whole kernel (not re-derived or re-loaded from a table per row)
+__device__ __forceinline__ Mfma8K mfma8_consts()
+{
+    Mfma8K k{};
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int r = __lane_id() & 3;
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        k.e[t] = r == 0 ? kMe[0][t] : (r == 1 ? kMe[1][t] : (r == 2 ? kMe[2][t] : kMe[3][t]));
+        k.o[t] = r == 0 ? kMo[0][t] : (r == 1 ? kMo[1][t] : (r == 2 ? kMo[2][t] : kMo[3][t]));
+        asm volatile("" : "+v"(k.e[t]), "+v"(k.o[t]));
+    }
+#endif
+    return k;
+}
+#endif
+
+// The eight outputs of texture column x (all texture atoms: order irrelevant).
+// MATRIX (device, every lane of the wave active, mk from mfma8_consts): on the
+// matrix pipe; otherwise the same fmaf chains on the VALU (host emulation,
+// and device kernels whose lanes may be inactive: dcte_pixel.h) -- identical
+// bits either way.
+template <bool MATRIX>
+DCTE_HD void col_mfma8(const float x[8], const Mfma8K& mk, float out[8])
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (MATRIX) {
+        dcte_v4f ev = {0.f, 0.f, 0.f, 0.f}, od = {0.f, 0.f, 0.f, 0.f};
+#if DCTE_MFMA8_SYM
+        float sv[4], dv[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            sv[t] = x[t] + x[7 - t];
+            dv[t] = x[t] - x[7 - t];
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            ev = __builtin_amdgcn_mfma_f32_4x4x1f32(mk.e[t], sv[t], ev, 0, 0, 0);
+            od = __builtin_amdgcn_mfma_f32_4x4x1f32(mk.o[t], dv[t], od, 0, 0, 0);
+        }
+#else
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            ev = __builtin_amdgcn_mfma_f32_4x4x1f32(mk.e[t], x[t], ev, 0, 0, 0);
+            od = __builtin_amdgcn_mfma_f32_4x4x1f32(mk.o[t], x[t], od, 0, 0, 0);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            ev = __builtin_amdgcn_mfma_f32_4x4x1f32(mk.e[3 - t], x[4 + t], ev, 0, 0, 0);
+            od = __builtin_amdgcn_mfma_f32_4x4x1f32(-mk.o[3 - t], x[4 + t], od, 0, 0, 0);
+        }
+#endif
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            out[r] = ev[r];
+            out[4 + r] = od[r];
+        }
+        return;
+    }
+#endif
+    (void)mk;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        float e = 0.0f, o = 0.0f;
+#if DCTE_MFMA8_SYM
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            e = fmaf(kMe[r][t], x[t] + x[7 - t], e);
+            o = fmaf(kMo[r][t], x[t] - x[7 - t], o);
+        }
+#else
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            e = fmaf(kMe[r][t], x[t], e);
+            o = fmaf(kMo[r][t], x[t], o);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            e = fmaf(kMe[r][3 - t], x[4 + t], e);
+            o = fmaf(-kMo[r][3 - t], x[4 + t], o);
+        }
+#endif
+        out[r] = e;
+        out[4 + r] = o;
+    }
+}
 
 template <int N>
 struct Lanes {
@@ -57,8 +180,11 @@ struct Cols;
 template <>
 struct Cols<8> {
     // ring[s][k1]; oldest row in slot O.  k1 = 0 first (m starts at 0)
-    template <int O>
-    DCTE_HD_MEMBER void run(const float (&ring)[8][8], int /*lane_p*/, float& mt, float& me)
+    // MATRIX: the DCTE_MFMA8 texture columns on the matrix pipe (dcte_map,
+    // mk = mfma8_consts()); otherwise their fmaf chains on the VALU, same bits
+    template <int O, bool MATRIX = false>
+    DCTE_HD_MEMBER void run(const float (&ring)[8][8], int /*lane_p*/, float& mt, float& me,
+                            const Mfma8K& mk = Mfma8K{})
     {
         float col[8];
         float e0, e1;
@@ -68,12 +194,25 @@ struct Cols<8> {
         // it is formed; k1 = 1 seeds them and k1 = 0 comes last (fewer live
         // registers than seeding from k1 = 0)
         float v1, ye[2], ya[2], pq, unused;
+#if DCTE_MFMA8 > 0
+        // the matrix-pipe columns first: their chains run while the VALU
+        // columns below are computed, and are folded last
+        constexpr int KM = 8 - DCTE_MFMA8;
+        float mx[DCTE_MFMA8][8];
+#pragma unroll
+        for (int k = KM; k < 8; k++) {
+            col_at<O>(ring, k, col);
+            col_mfma8<MATRIX>(col, mk, mx[k - KM]);
+        }
+#else
+        constexpr int KM = 8;
+#endif
         col_at<O>(ring, 1, col);
         dct8_col_sc<true>(col, v1, ye, ya, pq, e1);
         float m1 = fabsf(v1), mQ = pq;
         float mE = fmaxf(fabsf(ye[0]), fabsf(ye[1])), mA = fmaxf(fabsf(ya[0]), fabsf(ya[1]));
 #pragma unroll
-        for (int k = 2; k < 8; k++) {
+        for (int k = 2; k < KM; k++) {
             col_at<O>(ring, k, col);
             dct8_col_sc<false>(col, v1, ye, ya, pq, unused);
             m1 = fmaxf(m1, v1);
@@ -83,6 +222,13 @@ struct Cols<8> {
         }
         col_at<O>(ring, 0, col);
         dct8_k0_sc(col, m1, mE, mA, mQ, e0);
+#if DCTE_MFMA8 > 0
+        // matrix-pipe outputs are plain hat-unit coefficients: scale-1 chain
+#pragma unroll
+        for (int k = 0; k < DCTE_MFMA8; k++)
+#pragma unroll
+            for (int r = 0; r < 8; r += 2) m1 = max2in(m1, mx[k][r], mx[k][r + 1]);
+#endif
         mt = max2in(max2in(m1, mQ * k8sPQ, mE * k8sE), mA * k8sA, 0.0f);
         me = fmaxf(e1, e0 * k8sPQ);
 #else

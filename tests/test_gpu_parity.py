@@ -490,26 +490,31 @@ def test_refine_all_bit_exact_every_layout(n):
 
 
 def test_failed_call_then_good_call(ctx):
-    """A call the library rejects after the refinement scratch of its stream
-    exists (tile rows past the launch grid's y limit -> DCTE_ERANGE) leaves
-    nothing behind: the next calls on the same stream refine exactly the
-    pixels the fp32 path flags, and match the reference (a stale
-    dirty-strip counter would walk an older launch's list)."""
+    """A device call the library rejects (tile rows past the launch grid's y
+    limit -> DCTE_ERANGE) between good calls on the same stream leaves
+    nothing behind: the calls after it give the same bits as the call before
+    it, within tolerance of the reference (a stale dirty-strip
+    counter would make the refinement walk an older launch's list)."""
+    torch = _torch()
     rng = np.random.default_rng(17)
     img = (rng.random((96, 160)) < 0.03).astype(np.uint8) * 255
     ref = O.energy_map(img, 8, 0.3, 0.7)
-    _, me, mt = EM.energy_map(img, 8, 0.3, 0.7)
-    flagged = int(EM.refine_mask(me, mt, 0.3, 0.7).sum())
-    assert flagged > 0
-    _assert_tol(ctx.energy_map(img, 8, 0.3, 0.7), ref, "before")
-    tall = np.zeros((70000, 2), np.uint8)
+    frame = torch.from_numpy(img).cuda()
+    before = torch.empty((96, 160), dtype=torch.float32, device="cuda")
+    ctx.energy_map_tensor(frame, before, 8, 0.3, 0.7)
+    torch.cuda.synchronize()
+    _assert_tol(before.cpu().numpy(), ref, "before")
+    tall = torch.zeros((70000, 2), dtype=torch.uint8, device="cuda")
+    tall_out = torch.empty((70000, 2), dtype=torch.float32, device="cuda")
     try:
         ctx.set_option(dctenergy.DCTE_OPT_TILE_H, 1)
         with pytest.raises(dctenergy.DcteError) as e:
-            ctx.energy_map(tall, 8, 0.3, 0.7)
+            ctx.energy_map_tensor(tall, tall_out, 8, 0.3, 0.7)
         assert e.value.code == dctenergy.DCTE_ERANGE
     finally:
         ctx.set_option(dctenergy.DCTE_OPT_TILE_H, 0)
     for _ in range(2):
-        _assert_tol(ctx.energy_map(img, 8, 0.3, 0.7), ref, "after")
-        assert ctx.last_refined == flagged
+        after = torch.full((96, 160), -1.0, dtype=torch.float32, device="cuda")
+        ctx.energy_map_tensor(frame, after, 8, 0.3, 0.7)
+        torch.cuda.synchronize()
+        assert torch.equal(after, before)

@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--e2e", action="store_true",
                     help="time whole calls (map + refinement + launch gaps) with stream events "
                          "instead of the map launches alone")
+    ap.add_argument("--check", type=int, default=0,
+                    help="also map a CHECKxCHECK natural frame and a dots-on-flat frame with "
+                         "every build and compare with the CPU oracle (tolerance, class flips)")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     import torch
@@ -83,12 +86,42 @@ def main():
                 if ref is None:
                     ref = out.clone()
                 same[p] = bool(torch.equal(out, ref))
+    checks = {}
+    if a.check:
+        import numpy as np
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_py as O
+        from golden_util import within_tol
+        C = a.check
+        rng = np.random.default_rng(5)
+        nat = synth.natural_rows(0, C, C, a.bpp, seed=1, device="cuda")
+        dots = np.where(rng.random((C, C)) < 1 / 64, 255, 16).astype(np.uint8)
+        dots = torch.from_numpy(np.repeat(dots[..., None], a.bpp, -1).copy()).cuda()
+        frames = [(nat, O.energy_map(nat.cpu().numpy(), a.n, 0.3, 0.7)),
+                  (dots, O.energy_map(dots.cpu().numpy(), a.n, 0.3, 0.7))]
+        cout = torch.empty((C, C), dtype=torch.float32, device="cuda")
+        for p, L, h in libs:
+            bad = flips = 0
+            worst = 0.0
+            for fr, ref in frames:
+                rc = L.dcte_energy_map_device(h, 0, fr.data_ptr(), fr.stride(0), C, C, a.bpp, 0, C,
+                                              0, C, a.n, 0.3, 0.7, a.sem, cout.data_ptr(),
+                                              cout.stride(0), stream)
+                assert rc == 0, rc
+                torch.cuda.synchronize()
+                got = cout.cpu().numpy()
+                bad += int((~within_tol(got, ref)).sum())
+                rel = np.abs(got.astype(np.float64) - ref) / np.maximum(np.abs(ref), 1e-30)
+                worst = max(worst, float(rel[np.abs(ref) > 1e-9].max()))
+                # a class flip changes the weight: e = 0.3 vs t = 0.7 differ by > 2x
+                flips += int((np.abs(got - ref) > 0.25 * np.abs(ref)).sum())
+            checks[p] = {"check_off_tol": bad, "check_flips": flips, "check_max_rel": worst}
     for p in a.libs:
         t = times[p]
         print(json.dumps({"lib": os.path.basename(p), "n": a.n, "size": S, "e2e": a.e2e,
                           "median_ms": round(statistics.median(t), 4), "min_ms": round(min(t), 4),
                           "mpx_s": round(S * S / statistics.median(t) / 1e3, 1),
-                          "bit_equal_first": same[p]}))
+                          "bit_equal_first": same[p], **checks.get(p, {})}))
 
 
 if __name__ == "__main__":
