@@ -1065,6 +1065,180 @@ int dcte_carve(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t r
     return sync_bands(ctx, 1);
 }
 
+}  // extern "C"
+
+// ---- device mirror of a liblqr carver (the update_emap hook) ----
+struct dcte_carver {
+    dcte_ctx* ctx = nullptr;
+    int W0 = 0, H = 0, w = 0, bpp = 0, n = 0, r = 0, bw = 0;
+    float edges = 0, textures = 0;
+    size_t pitch = 0;
+    uint8_t* d_px = nullptr;   // carved frame (row pitch W0 * bpp)
+    float* d_map = nullptr;    // its energies (row pitch W0)
+    int* d_seam = nullptr;     // H
+    int* d_x0 = nullptr;       // H
+    float* d_be = nullptr;     // H x bw
+    uint8_t* d_bpx = nullptr;  // H x bw x bpp
+    std::vector<int> seam;     // host copy of the last seam
+};
+
+namespace {
+
+void carver_free(dcte_carver* c)
+{
+    if (!c) return;
+    if (!c->ctx->devs.empty() && hipSetDevice(c->ctx->devs[0].id) == hipSuccess) {
+        if (c->ctx->devs[0].stream) (void)hipStreamSynchronize(c->ctx->devs[0].stream);
+        for (void* p : {(void*)c->d_px, (void*)c->d_map, (void*)c->d_seam, (void*)c->d_x0,
+                        (void*)c->d_be, (void*)c->d_bpx})
+            if (p) (void)hipFree(p);
+    }
+    delete c;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dcte_carver_create(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride,
+                       int n, float edges, float textures, int transposed, float* map_out,
+                       dcte_carver** out)
+{
+    DeviceGuard guard_;
+    if (!ctx || !out) return DCTE_EINVAL;
+    *out = nullptr;
+    DCTE_ARG(ctx, px && valid_n(n) && valid_sem_bpp(DCTE_LQR, bpp) && w > 0 && h > 0);
+    DCTE_ARG(ctx, rowstride >= (size_t)w * bpp);
+    Device& d = ctx->devs[0];
+    int rc = ensure_stream(ctx, d);
+    if (rc) return rc;
+    hipStream_t s = d.stream;
+    dcte_carver* c = new (std::nothrow) dcte_carver;
+    if (!c) return DCTE_ENOMEM;
+    c->ctx = ctx;
+    c->W0 = transposed ? h : w;
+    c->H = transposed ? w : h;
+    c->w = c->W0;
+    c->bpp = bpp;
+    c->n = n;
+    c->r = n / 2;                    // the radius the plug-in registers (src/render.c:314-315)
+    c->bw = 4 * c->r + 4;
+    c->edges = edges;
+    c->textures = textures;
+    c->pitch = (size_t)c->W0 * bpp;
+    c->seam.assign(c->H, 0);
+    const size_t fbytes = c->pitch * (size_t)c->H;
+    auto fail = [&](hipError_t e, const char* where) {
+        int code = hip_fail(ctx, e, where);
+        carver_free(c);
+        return code;
+    };
+    hipError_t e;
+    if ((e = hipMalloc(&c->d_px, fbytes)) != hipSuccess) return fail(e, "hipMalloc frame");
+    if ((e = hipMalloc(&c->d_map, sizeof(float) * (size_t)c->W0 * c->H)) != hipSuccess) return fail(e, "hipMalloc map");
+    if ((e = hipMalloc(&c->d_seam, sizeof(int) * (size_t)c->H)) != hipSuccess) return fail(e, "hipMalloc seam");
+    if ((e = hipMalloc(&c->d_x0, sizeof(int) * (size_t)c->H)) != hipSuccess) return fail(e, "hipMalloc x0");
+    if ((e = hipMalloc(&c->d_be, sizeof(float) * (size_t)c->H * c->bw)) != hipSuccess) return fail(e, "hipMalloc band");
+    if ((e = hipMalloc(&c->d_bpx, (size_t)c->H * c->bw * bpp)) != hipSuccess) return fail(e, "hipMalloc band px");
+    const size_t spitch = (size_t)w * bpp;
+    if (transposed) {
+        uint8_t* d_tmp = nullptr;
+        if ((e = hipMalloc(&d_tmp, fbytes)) != hipSuccess) return fail(e, "hipMalloc staging");
+        e = hipMemcpy2DAsync(d_tmp, spitch, px, rowstride, spitch, h, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess)
+            e = dcte::launch_transpose_u8(d_tmp, (long long)spitch, h, w, bpp, c->d_px, (long long)c->pitch, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        (void)hipFree(d_tmp);
+        if (e != hipSuccess) return fail(e, "upload (transposed)");
+    } else if ((e = hipMemcpy2DAsync(c->d_px, c->pitch, px, rowstride, spitch, h,
+                                     hipMemcpyHostToDevice, s)) != hipSuccess) {
+        return fail(e, "upload");
+    }
+    rc = run_device(ctx, d, c->d_px, (long long)c->pitch, c->W0, c->H, bpp, 0, c->H, 0, c->H, n,
+                    edges, textures, DCTE_LQR, c->d_map, c->W0, s);
+    if (rc == DCTE_OK && map_out &&
+        (e = hipMemcpyAsync(map_out, c->d_map, sizeof(float) * (size_t)c->W0 * c->H,
+                            hipMemcpyDeviceToHost, s)) != hipSuccess)
+        rc = hip_fail(ctx, e, "map download");
+    if (rc == DCTE_OK && (e = hipStreamSynchronize(s)) != hipSuccess) rc = hip_fail(ctx, e, "sync");
+    if (rc) {
+        carver_free(c);
+        return rc;
+    }
+    *out = c;
+    return DCTE_OK;
+}
+
+int dcte_carver_width(const dcte_carver* c) { return c ? c->w : 0; }
+int dcte_carver_height(const dcte_carver* c) { return c ? c->H : 0; }
+int dcte_carver_band_width(const dcte_carver* c) { return c ? c->bw : 0; }
+
+int dcte_carver_step(dcte_carver* c, int* seam, int* band_x0, float* band_e, uint8_t* band_px)
+{
+    DeviceGuard guard_;
+    if (!c) return DCTE_EINVAL;
+    dcte_ctx* ctx = c->ctx;
+    DCTE_ARG(ctx, c->w >= 2);
+    Device& d = ctx->devs[0];
+    int rc = ensure_stream(ctx, d);
+    if (rc) return rc;
+    hipStream_t s = d.stream;
+    // the seam first, checked on the host before anything moves (a search
+    // that timed out is re-run band-wise, as dcte_seam_find does)
+    for (;;) {
+        rc = dcte_seam_find_device(ctx, 0, c->d_map, c->W0, c->w, c->H, c->d_seam, s);
+        if (rc) return rc;
+        DCTE_HIP(ctx, hipMemcpyAsync(c->seam.data(), c->d_seam, sizeof(int) * (size_t)c->H,
+                                     hipMemcpyDeviceToHost, s));
+        DCTE_HIP(ctx, hipStreamSynchronize(s));
+        if (c->seam[0] >= 0) break;
+        if (!dp_fall_back(d, s)) {
+            ctx->last_error = "seam search timed out waiting for a neighbour tile";
+            return DCTE_EHIP;
+        }
+    }
+    rc = dcte_seam_carve_device(ctx, 0, c->d_px, (long long)c->pitch, c->w, c->H, c->bpp, c->d_seam,
+                                c->d_map, c->W0, c->d_px, (long long)c->pitch, c->d_map, c->W0,
+                                c->n, c->edges, c->textures, DCTE_LQR, s);
+    if (rc) {
+        drain(ctx, 1);
+        return rc;
+    }
+    c->w--;
+    dcte::BandParams b{};
+    b.seam = c->d_seam;
+    b.w = c->w;
+    b.h = c->H;
+    b.r = c->r;
+    b.bw = c->bw;
+    b.bpp = c->bpp;
+    b.map = c->d_map;
+    b.map_stride = c->W0;
+    b.px = c->d_px;
+    b.rowstride = (long long)c->pitch;
+    b.x0 = c->d_x0;
+    b.e = c->d_be;
+    b.pxb = c->d_bpx;
+    DCTE_HIP(ctx, dcte::launch_band_gather(b, s));
+    if (seam) memcpy(seam, c->seam.data(), sizeof(int) * (size_t)c->H);
+    if (band_x0)
+        DCTE_HIP(ctx, hipMemcpyAsync(band_x0, c->d_x0, sizeof(int) * (size_t)c->H, hipMemcpyDeviceToHost, s));
+    if (band_e)
+        DCTE_HIP(ctx, hipMemcpyAsync(band_e, c->d_be, sizeof(float) * (size_t)c->H * c->bw,
+                                     hipMemcpyDeviceToHost, s));
+    if (band_px)
+        DCTE_HIP(ctx, hipMemcpyAsync(band_px, c->d_bpx, (size_t)c->H * c->bw * c->bpp,
+                                     hipMemcpyDeviceToHost, s));
+    DCTE_HIP(ctx, hipStreamSynchronize(s));
+    return DCTE_OK;
+}
+
+void dcte_carver_destroy(dcte_carver* c)
+{
+    DeviceGuard guard_;
+    carver_free(c);
+}
+
 int dcte_energy_map(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride,
                     int n, float edges, float textures, int semantics, int transposed, float* out)
 {

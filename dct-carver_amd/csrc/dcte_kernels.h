@@ -87,6 +87,19 @@ struct SeamParams {
     unsigned fix_cap;
 };
 
+// Band of a carver step (dcte_band_gather, dcte_seam.hip)
+struct BandParams {
+    const int* seam;         // h columns just removed (frame coordinates before the step)
+    int w, h, r, bw, bpp;    // carved width, rows, update radius, band width
+    const float* map;        // carved frame's energies
+    long long map_stride;
+    const uint8_t* px;       // carved frame
+    long long rowstride;
+    int* x0;                 // h: first band column per row
+    float* e;                // h x bw energies
+    uint8_t* pxb;            // h x bw x bpp pixels
+};
+
 // Energies of given windows (dcte_windows): count windows of N x N doubles,
 // the reference's data[i][j] layout, in the reference's arithmetic.
 struct WinParams {
@@ -125,6 +138,7 @@ hipError_t launch_fix(const FixParams& p, hipStream_t s);
 hipError_t launch_fix_tiles(int n, int bpp, int sem, const TileFixParams& p, hipStream_t s);
 hipError_t launch_seam_carve(const SeamParams& p, hipStream_t s);
 hipError_t launch_points(const SeamParams& p, hipStream_t s);
+hipError_t launch_band_gather(const BandParams& p, hipStream_t s);
 hipError_t launch_windows(const WinParams& p, hipStream_t s);
 hipError_t launch_seam_find(const DpParams& p, hipStream_t s, bool resident);
 int dp_tile_cols();

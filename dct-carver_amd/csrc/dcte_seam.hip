@@ -225,6 +225,35 @@ __global__ __launch_bounds__(256) void dcte_points(const SeamParams p)
     emit_pixel(p, mt, me, p.map_out + k, (unsigned)k);
 }
 
+// Band of one carver step (dcte_carver_step): after seam s removed from a
+// frame, row y of the carved w-wide frame keeps, from column x0[y] on, `bw`
+// energies and pixels -- x0[y] = lo - R - 1 clamped to [0, max(0, w - bw)],
+// lo = min of s over rows y - R .. y + R: every pixel whose liblqr update
+// window (radius R) can reach the seam [liblqr, unverified] lies inside
+// (the seam moves <= 1 column per row, so bw = 4 R + 4 covers it).
+// One wave per row.
+__global__ __launch_bounds__(64) void dcte_band_gather(const BandParams p)
+{
+    const int y = blockIdx.x, l = threadIdx.x;
+    int lo = p.w;
+    for (int j = -p.r; j <= p.r; j++) lo = min(lo, p.seam[clamp_px(y + j, 0, p.h - 1)]);
+    const int x0 = clamp_px(lo - p.r - 1, 0, max(0, p.w - p.bw));
+    if (l == 0) p.x0[y] = x0;
+    for (int k = l; k < p.bw; k += 64) {
+        const int x = min(x0 + k, p.w - 1);
+        p.e[(long long)y * p.bw + k] = p.map[(long long)y * p.map_stride + x];
+        for (int c = 0; c < p.bpp; c++)
+            p.pxb[((long long)y * p.bw + k) * p.bpp + c] = p.px[(long long)y * p.rowstride + (long long)x * p.bpp + c];
+    }
+}
+
+hipError_t launch_band_gather(const BandParams& p, hipStream_t s)
+{
+    if (p.h <= 0) return hipSuccess;
+    hipLaunchKernelGGL(dcte_band_gather, dim3(p.h), dim3(64), 0, s, p);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ launchers
 #define DCTE_SEM_BPP_SWITCH(KERNEL, N, grid, block, s, p)                                        \
     do {                                                                                        \

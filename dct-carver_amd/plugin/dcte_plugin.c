@@ -4,6 +4,7 @@
  * times over, and the single-device path is the one the GPU tests run. */
 #include "dcte_plugin.h"
 
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -28,9 +29,22 @@ static dcte_ctx *plugin_ctx(void)
     return g_ctx_status == DCTE_OK ? g_ctx : NULL;
 }
 
-int dcte_plugin_build(dcte_map_cache *c, const uint8_t *px, int w, int h, int bpp,
-                      size_t rowstride, int blocksize, float edges, float textures,
-                      int with_transposed)
+static void release_hook(dcte_map_cache *c)
+{
+    dcte_carver_destroy(c->mirror);
+    free(c->band_x0);
+    free(c->band_e);
+    free(c->band_px);
+    c->mirror = NULL;
+    c->band_x0 = NULL;
+    c->band_e = NULL;
+    c->band_px = NULL;
+    c->band_valid = c->hook_ok = 0;
+}
+
+int dcte_plugin_build_ex(dcte_map_cache *c, const uint8_t *px, int w, int h, int bpp,
+                         size_t rowstride, int blocksize, float edges, float textures,
+                         int with_transposed, unsigned flags)
 {
     if (!c) return DCTE_EINVAL;
     memset(c, 0, sizeof(*c));
@@ -39,9 +53,35 @@ int dcte_plugin_build(dcte_map_cache *c, const uint8_t *px, int w, int h, int bp
     if (w <= 0 || h <= 0) return c->status = DCTE_EINVAL;
     c->map = (float *)malloc(sizeof(float) * (size_t)w * (size_t)h);
     if (!c->map) return c->status = DCTE_ENOMEM;
-    c->status = dcte_energy_map(ctx, px, w, h, bpp, rowstride, blocksize, edges, textures,
-                                DCTE_LQR, 0, c->map);
-    if (c->status == DCTE_OK && with_transposed) {
+    const int ho = with_transposed ? 1 : 0;
+    if ((flags & DCTE_PLUGIN_SEAM_HOOK) && (bpp == 1 || bpp == 3)) {
+        /* the mirror maps the frame of the resize orientation itself */
+        float *first = NULL;
+        if (ho) first = c->map_t = (float *)malloc(sizeof(float) * (size_t)w * (size_t)h);
+        else first = c->map;
+        if (first && dcte_carver_create(ctx, px, w, h, bpp, rowstride, blocksize, edges, textures, ho,
+                                        first, &c->mirror) == DCTE_OK) {
+            c->hook_orientation = ho;
+            c->mw = dcte_carver_width(c->mirror);
+            c->mh = dcte_carver_height(c->mirror);
+            c->bw = dcte_carver_band_width(c->mirror);
+            c->bpp = bpp;
+            c->band_x0 = (int *)malloc(sizeof(int) * (size_t)c->mh);
+            c->band_e = (float *)malloc(sizeof(float) * (size_t)c->mh * c->bw);
+            c->band_px = (unsigned char *)malloc((size_t)c->mh * c->bw * bpp);
+            c->hook_ok = c->band_x0 && c->band_e && c->band_px;
+            if (!c->hook_ok) release_hook(c);
+        }
+        if (!c->mirror && ho) {           /* no mirror: the map_t build below */
+            free(c->map_t);
+            c->map_t = NULL;
+        }
+    }
+    c->status = DCTE_OK;
+    if (!(c->mirror && ho == 0))
+        c->status = dcte_energy_map(ctx, px, w, h, bpp, rowstride, blocksize, edges, textures,
+                                    DCTE_LQR, 0, c->map);
+    if (c->status == DCTE_OK && with_transposed && !c->map_t) {
         c->map_t = (float *)malloc(sizeof(float) * (size_t)w * (size_t)h);
         c->status = c->map_t ? dcte_energy_map(ctx, px, w, h, bpp, rowstride, blocksize, edges,
                                                textures, DCTE_LQR, 1, c->map_t)
@@ -49,6 +89,7 @@ int dcte_plugin_build(dcte_map_cache *c, const uint8_t *px, int w, int h, int bp
     }
     if (c->status != DCTE_OK) {
         int st = c->status;
+        release_hook(c);
         free(c->map);
         free(c->map_t);
         memset(c, 0, sizeof(*c));
@@ -58,6 +99,14 @@ int dcte_plugin_build(dcte_map_cache *c, const uint8_t *px, int w, int h, int bp
     c->h = h;
     c->valid = 1;
     return DCTE_OK;
+}
+
+int dcte_plugin_build(dcte_map_cache *c, const uint8_t *px, int w, int h, int bpp,
+                      size_t rowstride, int blocksize, float edges, float textures,
+                      int with_transposed)
+{
+    return dcte_plugin_build_ex(c, px, w, h, bpp, rowstride, blocksize, edges, textures,
+                                with_transposed, 0u);
 }
 
 int dcte_plugin_lookup(const dcte_map_cache *c, int x, int y, int w, int h, int orientation,
@@ -75,9 +124,56 @@ int dcte_plugin_lookup(const dcte_map_cache *c, int x, int y, int w, int h, int 
     return 0;
 }
 
+/* liblqr's LQR_ER_LUMA of a pixel [liblqr, unverified] (the formula the
+ * reading window returns; src/render.c:315) */
+static double lqr_luma(const unsigned char *q, int bpp)
+{
+    if (bpp == 1) return (double)q[0] / 255;
+    return 0.2126 * ((double)q[0] / 255) + 0.7152 * ((double)q[1] / 255) +
+           0.0722 * ((double)q[2] / 255);
+}
+
+int dcte_plugin_lookup_hook(dcte_map_cache *c, int x, int y, int w, int h, int orientation,
+                            double center_luma, float *out)
+{
+    if (dcte_plugin_lookup(c, x, y, w, h, orientation, out)) {
+        if (c) c->served_map++;
+        return 1;
+    }
+    if (!c || !c->valid || !c->hook_ok || orientation != c->hook_orientation || h != c->mh ||
+        x < 0 || y < 0 || x >= w || y >= h)
+        return 0;
+    /* liblqr carved since the mirror's last step: carve the same seams */
+    while (w < c->mw) {
+        if (dcte_carver_step(c->mirror, NULL, c->band_x0, c->band_e, c->band_px) != DCTE_OK) {
+            release_hook(c);
+            c->missed++;
+            return 0;
+        }
+        c->mw--;
+        c->steps++;
+        c->band_valid = 1;
+    }
+    const int k = x - c->band_x0[y];
+    if (w != c->mw || !c->band_valid || k < 0 || k >= c->bw) {
+        c->missed++;
+        return 0;
+    }
+    const size_t at = (size_t)y * c->bw + (size_t)k;
+    if (!isnan(center_luma) && fabs(lqr_luma(c->band_px + at * c->bpp, c->bpp) - center_luma) > 1e-9) {
+        release_hook(c);       /* the mirror diverged from liblqr's image */
+        c->missed++;
+        return 0;
+    }
+    *out = c->band_e[at];
+    c->served_band++;
+    return 1;
+}
+
 void dcte_plugin_release(dcte_map_cache *c)
 {
     if (!c) return;
+    release_hook(c);
     free(c->map);
     free(c->map_t);
     memset(c, 0, sizeof(*c));

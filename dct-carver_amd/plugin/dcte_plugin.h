@@ -21,13 +21,29 @@
 extern "C" {
 #endif
 
+struct dcte_carver;
+
 typedef struct {
     float *map;      /* w*h energies of the frame (orientation 0), owned */
     float *map_t;    /* h*w energies of the transposed frame (orientation 1), or NULL */
     int w, h;        /* frame size */
     int valid;
     int status;      /* DCTE_* code of the last build */
+    /* opt-in seam hook (DCTE_PLUGIN_SEAM_HOOK): a device
+     * mirror of the carver that replays each seam liblqr carves and hands
+     * back the energies around it, so update_emap's callbacks are served too */
+    struct dcte_carver *mirror;
+    int hook_orientation;  /* the orientation liblqr resizes in */
+    int hook_ok;           /* 0 once the mirror lost track of liblqr's image */
+    int mw, mh, bpp, bw;   /* mirror's current width, height; bytes per pixel; band width */
+    int band_valid;
+    int *band_x0;          /* mh: first band column per row */
+    float *band_e;         /* mh x bw energies of the last step's band */
+    unsigned char *band_px;/* mh x bw x bpp pixels (divergence check) */
+    long long served_map, served_band, missed, steps;
 } dcte_map_cache;
+
+#define DCTE_PLUGIN_SEAM_HOOK 1u
 
 /* Build the map(s) for the frame handed to lqr_carver_new (src/render.c:312):
  * orientation 0 always, and the transposed frame's map too when
@@ -39,11 +55,30 @@ int dcte_plugin_build(dcte_map_cache *c, const uint8_t *px, int w, int h, int bp
                       size_t rowstride, int blocksize, float edges, float textures,
                       int with_transposed);
 
+/* dcte_plugin_build with flags: DCTE_PLUGIN_SEAM_HOOK also sets up the
+ * device mirror of the carver for the orientation liblqr will resize in
+ * (with_transposed: vertical, 1; else 0).  Without a GPU, or when the mirror
+ * cannot be set up, the build behaves as dcte_plugin_build. */
+int dcte_plugin_build_ex(dcte_map_cache *c, const uint8_t *px, int w, int h, int bpp,
+                         size_t rowstride, int blocksize, float edges, float textures,
+                         int with_transposed, unsigned flags);
+
 /* 1 and *out = energy when (x, y) of a w x h carver in `orientation` is
  * served from a map (orientation 0: the frame's size; 1: the transposed
  * frame's size, if that map was built); 0 otherwise. */
 int dcte_plugin_lookup(const dcte_map_cache *c, int x, int y, int w, int h,
                        int orientation, float *out);
+
+/* The same, plus the seam hook: when the carver has become narrower than the
+ * mirror (liblqr carved a seam), the mirror carves the same seam on the GPU
+ * and pixels of its update band are served too.  center_luma: what the
+ * callback's reading window holds at offset (0, 0) (lqr_rwindow_read, as
+ * src/render.c:150 reads it), checked against the mirror's pixel; a mismatch
+ * means the mirror no longer follows liblqr's image and switches the hook off
+ * for this carver (NaN skips the check).  Misses return 0: the callback then
+ * runs its original per-window code. */
+int dcte_plugin_lookup_hook(dcte_map_cache *c, int x, int y, int w, int h, int orientation,
+                            double center_luma, float *out);
 
 void dcte_plugin_release(dcte_map_cache *c);
 

@@ -240,6 +240,38 @@ int dcte_carve(dcte_ctx *ctx, const uint8_t *px, int w, int h, int bpp, size_t r
                int n, float edges, float textures, int semantics, int seams, int transposed,
                uint8_t *out, int *seam_cols);
 
+/* ---- device mirror of a liblqr carver -------------------
+ * The update_emap hook of the plug-in: after the first
+ * build, liblqr's resize loop (lqr_carver_resize, src/render.c:377) carves one
+ * seam at a time and asks the energy callback again only around it
+ * (update_emap) [liblqr, unverified].  A dcte_carver holds the carver's frame
+ * and energy map in HBM and replays that loop: each step finds the seam
+ * liblqr's DP picks on the same energies (dcte_seam_find_device: delta_x 1,
+ * rigidity 0, src/render.c:313), carves it and updates the map
+ * (dcte_seam_carve_device), then hands back the energies -- and the pixels,
+ * so the caller can check that it follows liblqr's image -- of a band around
+ * the seam: row y holds band_width columns from band_x0[y] on of the carved
+ * frame, covering every pixel whose radius-N/2 window reaches the seam.
+ * Every value equals dcte_energy_map of the carved frame at that pixel.
+ * liblqr semantics (DCTE_LQR), bpp 1 or 3.
+ *
+ * dcte_carver_create: uploads px (w x h; transposed = 1 mirrors a carver that
+ *   liblqr transposed for a vertical resize: the frame is then h wide) and
+ *   maps it; map_out (optional) receives that first map (width x height
+ *   floats of the mirrored frame).
+ * dcte_carver_step: one seam.  seam (height ints, columns in the frame before
+ *   the step), band_x0 (height ints), band_e (height x band_width floats),
+ *   band_px (height x band_width x bpp bytes): each optional. */
+typedef struct dcte_carver dcte_carver;
+int dcte_carver_create(dcte_ctx *ctx, const uint8_t *px, int w, int h, int bpp, size_t rowstride,
+                       int n, float edges, float textures, int transposed, float *map_out,
+                       dcte_carver **out);
+int dcte_carver_step(dcte_carver *c, int *seam, int *band_x0, float *band_e, uint8_t *band_px);
+int dcte_carver_width(const dcte_carver *c);       /* current width of the mirrored frame */
+int dcte_carver_height(const dcte_carver *c);
+int dcte_carver_band_width(const dcte_carver *c);  /* 2 N + 4 */
+void dcte_carver_destroy(dcte_carver *c);
+
 /* ---- energy image as 8-bit grey ----------------------
  * DCTE_NORM_PREVIEW: normalize_image (src/render.c:81-109, DOUBLE2GUCHAR of
  *   src/render.h:6): ROUND(255*(E-min)/(max-min)) in double, replicated to

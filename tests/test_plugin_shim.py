@@ -36,6 +36,12 @@ def fake():
                                       ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                       ctypes.POINTER(ctypes.c_longlong),
                                       ctypes.POINTER(ctypes.c_int)]
+        L.fake_resize.restype = ctypes.c_int
+        L.fake_resize.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_int)]
         _lib = L
     return _lib
 
@@ -52,6 +58,91 @@ def build_emap(img, n, e, t, use_gpu, removed=0, transposed=False):
                                 ctypes.byref(status))
     assert rc == 0
     return out, calls.value, status.value
+
+
+def resize(img, n, e, t, seams, use_gpu, hook, transposed=False, perturb=False):
+    """fake liblqr resize loop (tests/fake_lqr: energy build, then per seam DP,
+    carve, update_emap through the patched callback) -> dict."""
+    img = np.ascontiguousarray(img)
+    h, w = img.shape[:2]
+    bpp = 1 if img.ndim == 2 else img.shape[2]
+    fw, fh = (h, w) if transposed else (w, h)
+    emap = np.empty((fh, fw - seams), np.float32)
+    px = np.empty((fh, fw - seams) + img.shape[2:], np.uint8)
+    seam_cols = np.empty((max(seams, 1), fh), np.int32)
+    counts = (ctypes.c_longlong * 6)()
+    status = ctypes.c_int()
+    rc = fake().fake_resize(img.ctypes.data, w, h, bpp, n, e, t, int(use_gpu), int(hook), seams,
+                            int(transposed), int(perturb), emap.ctypes.data, px.ctypes.data,
+                            seam_cols.ctypes.data, counts, ctypes.byref(status))
+    assert rc == 0
+    c = list(counts)
+    return {"emap": emap, "px": px, "seams": seam_cols[:seams], "callbacks": c[0],
+            "fallback": c[1], "served_map": c[2], "served_band": c[3], "steps": c[4], "update_ns": c[5],
+            "status": status.value, "initial": fw * fh}
+
+
+def test_resize_loop_without_gpu_is_the_reference():
+    """CPU: no device -> every callback of the build and of every update_emap
+    runs the original per-window code, and the final energies equal the
+    reference map of the carved image exactly (the update band liblqr
+    re-evaluates covers every pixel whose window the seam touched)."""
+    if dctenergy.device_count() > 0:
+        pytest.skip("device visible; covered by the GPU test")
+    img = load_input("natural_rgb_73x59.npy")
+    for n, transposed in ((8, False), (4, True), (16, False)):
+        r = resize(img, n, 0.15, 0.85, 6, use_gpu=True, hook=True, transposed=transposed)
+        assert r["status"] == dctenergy.DCTE_ENODEV
+        assert r["fallback"] == r["callbacks"] > r["initial"]
+        assert r["served_map"] == r["served_band"] == r["steps"] == 0
+        assert np.array_equal(r["emap"], O.energy_map(r["px"], n, 0.15, 0.85))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,transposed", [(8, False), (8, True), (4, False), (16, False), (2, True)])
+def test_seam_hook_serves_update_emap(n, transposed):
+    """The update_emap hook: with it every callback of a
+    liblqr resize -- the build and every seam's update band -- is answered by
+    the GPU (no per-window fallback), and the energies liblqr ends with are
+    bit-identical to the GPU map of the carved image (within tolerance of the
+    reference); without it only the build is served."""
+    img = load_input("natural_rgb_97x41.npy")
+    seams = 9
+    plain = resize(img, n, 0.15, 0.85, seams, use_gpu=True, hook=False, transposed=transposed)
+    hooked = resize(img, n, 0.15, 0.85, seams, use_gpu=True, hook=True, transposed=transposed)
+    for r in (plain, hooked):
+        assert r["status"] == dctenergy.DCTE_OK
+        assert within_tol(r["emap"], O.energy_map(r["px"], n, 0.15, 0.85)).all()
+    assert plain["served_map"] == plain["initial"]
+    assert plain["fallback"] == plain["callbacks"] - plain["initial"] > 0
+    assert hooked["fallback"] == 0 and hooked["steps"] == seams
+    assert hooked["served_map"] + hooked["served_band"] == hooked["callbacks"]
+    with dctenergy.Context(ngpus=1) as ctx:
+        assert np.array_equal(hooked["emap"], ctx.energy_map(hooked["px"], n, 0.15, 0.85))
+    print(n, transposed, "served without hook", plain["initial"] / plain["callbacks"],
+          "with hook", 1.0)
+
+
+@pytest.mark.gpu
+def test_seam_hook_follows_liblqr_and_lets_go_on_divergence():
+    """The fake liblqr's seams are the ones the GPU search finds on the GPU
+    maps of the successively carved frames (the mirror carves the same
+    pixels); and when liblqr's image is not the frame the mirror carves
+    (perturbed after the build), the centre-pixel check switches the hook
+    off at the first update callback and the original code answers."""
+    img = load_input("natural_rgb_97x41.npy")
+    r = resize(img, 8, 0.3, 0.7, 5, use_gpu=True, hook=True)
+    with dctenergy.Context(ngpus=1) as ctx:
+        px = np.ascontiguousarray(img)
+        for k in range(5):
+            s = ctx.seam_find(ctx.energy_map(px, 8, 0.3, 0.7))
+            assert np.array_equal(s, r["seams"][k])
+            px = np.ascontiguousarray(np.stack([np.delete(px[y], s[y], axis=0)
+                                                for y in range(px.shape[0])]))
+    assert np.array_equal(px, r["px"])
+    d = resize(img, 8, 0.3, 0.7, 5, use_gpu=True, hook=True, perturb=True)
+    assert d["steps"] == 1 and d["served_band"] == 0
+    assert d["fallback"] == d["callbacks"] - d["initial"] > 0
 
 
 @pytest.mark.parametrize("n", [2, 4, 8, 16])
