@@ -21,6 +21,7 @@ struct MapParams {
     int y0, y1;              // output rows (global)
     int tile_h;              // output rows per workgroup
     int fair;                // > 0: priority levels a workgroup steps down through its tile
+    int wide;                // N = 8: 1024-column tiles of 1024-thread workgroups (Geo WIDE)
     float* out;              // row y at out + (y - y0) * out_stride
     long long out_stride;    // floats
     float we, wt;            // edges / textures weights, pre-scaled to luma units
@@ -47,6 +48,7 @@ struct TileFixParams {
     double ct[4];            // makect twiddles (N = 2, 4)
     unsigned* fix_total;     // += pixels refined (host-path diagnostic), or null
     int tiles_x;             // map grid width in tiles
+    int tile_w;              // map tile width in columns (map_tile_w)
 };
 
 struct FixParams {
@@ -147,10 +149,10 @@ int dp_super_bands();
 int dp_max_tiles(int device);
 
 // geometry the launcher uses (exported for tests / bench)
-int map_tile_w(int n);
+int map_tile_w(int n, bool wide = false);
 int map_default_tile_h(int n);
-int map_tiles_x(int n, int w);                 // map grid (tiles) of a launch
+int map_tiles_x(int n, int w, bool wide = false);   // map grid (tiles) of a launch
 int map_tiles_y(int n, int rows, int tile_h);
-int map_strips_per_tile(int n);
+int map_strips_per_tile(int n, bool wide = false);
 
 }  // namespace dcte

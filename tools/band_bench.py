@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--tile-h", type=int, default=0)
     ap.add_argument("--lib", default=None, help="libdctenergy_hip.so to load (A/B)")
+    ap.add_argument("--wide", default="0,1",
+                    help="DCTE_OPT_WIDE_BANDS settings to compare, interleaved (e.g. 0,1)")
+    ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
     if a.lib:
         os.environ["DCTE_LIB"] = os.path.abspath(a.lib)
@@ -45,23 +48,32 @@ def main():
                                   n, 0.3, 0.7, out[y0 - Y0:].data_ptr(), out.stride(0), s.cuda_stream)
         pats = {"one launch": [(Y0, Y1)],
                 "interior + 2 edge launches (bench.py world > 1)": [(Y0 + hl, Y1 - hr), (Y0, Y0 + hl), (Y1 - hr, Y1)]}
-        for name, ranges in pats.items():
-            for _ in range(5):
-                for r in ranges:
-                    run(*r)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            torch.cuda.synchronize()
-            e0.record(s)
-            h0 = time.perf_counter()
-            for _ in range(a.iters):
-                for r in ranges:
-                    run(*r)
-            host_ms = (time.perf_counter() - h0) * 1e3 / a.iters
-            e1.record(s)
-            torch.cuda.synchronize()
-            ms = e0.elapsed_time(e1) / a.iters
-            print(json.dumps({"pattern": name, "lib": os.path.basename(a.lib or "default"), "rows": R, "width": W, "n": n, "tile_h": a.tile_h,
-                              "ms_per_step": round(ms, 4), "host_ms_per_step": round(host_ms, 4),
+        wides = [int(v) for v in a.wide.split(",")]
+        res = {}
+        for rnd in range(a.rounds):
+            for wide in wides:
+                ctx.set_option(dctenergy.DCTE_OPT_WIDE_BANDS, wide)
+                for name, ranges in pats.items():
+                    for _ in range(5):
+                        for r in ranges:
+                            run(*r)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    torch.cuda.synchronize()
+                    e0.record(s)
+                    h0 = time.perf_counter()
+                    for _ in range(a.iters):
+                        for r in ranges:
+                            run(*r)
+                    host_ms = (time.perf_counter() - h0) * 1e3 / a.iters
+                    e1.record(s)
+                    torch.cuda.synchronize()
+                    res.setdefault((wide, name), []).append((e0.elapsed_time(e1) / a.iters, host_ms))
+        for (wide, name), v in res.items():
+            ms = sorted(t for t, _ in v)[len(v) // 2]
+            print(json.dumps({"pattern": name, "wide": wide, "lib": os.path.basename(a.lib or "default"),
+                              "rows": R, "width": W, "n": n, "tile_h": a.tile_h,
+                              "ms_per_step": round(ms, 4),
+                              "host_ms_per_step": round(sorted(h for _, h in v)[len(v) // 2], 4),
                               "mpx_s": round(R * W / ms / 1e3, 1)}), flush=True)
 
 

@@ -38,8 +38,8 @@ def main():
             "frame": f"{w}x{h} RGB", "n": a.n, "seams": a.seams, "transposed": a.transposed,
             "hook": hook, "callbacks": r["callbacks"], "build_callbacks": r["initial"],
             "update_callbacks": upd, "update_callbacks_per_seam": round(upd / a.seams, 1),
-            "served_gpu": r["served_map"] + r["served_band"],
-            "served_frac": round((r["served_map"] + r["served_band"]) / r["callbacks"], 4),
+            "served_gpu": r["callbacks"] - r["fallback"],
+            "served_frac": round((r["callbacks"] - r["fallback"]) / r["callbacks"], 4),
             "fallback": r["fallback"], "mirror_steps": r["steps"],
             "update_ms_per_seam": round(r["update_ns"] / 1e6 / a.seams, 3)}), flush=True)
 
