@@ -584,21 +584,27 @@ __device__ __forceinline__ void lastmax_group(const double* v, int l, double& m,
 // registers (N <= 8): ddct8x8s along the first index, then the second;
 // ddct2d (N = 2, 4) the second index first.  The scan keeps the LAST maximum
 // (src/dct.c:103, "max <= currval"); edge atoms (0,1), (1,0) (src/dct.c:18-25).
-template <int N>
+#ifndef DCTE_FIX_IL
+#define DCTE_FIX_IL 1    // N = 8 register path: 8-point steps the scheduler may interleave
+#endif
+// FIRST = false: the caller already ran the first pass (dcte_fix_dense8)
+template <int N, int IL = DCTE_FIX_IL, bool FIRST = true>
 __device__ __forceinline__ void refine_regs(double (&d)[N * N], const double* ct, double& m, bool& edge)
 {
     if constexpr (N == 8) {
-        // one 8-point step at a time: interleaving all eight would need their
+        // IL 8-point steps at a time: interleaving all eight would need their
         // temporaries live beside the 64-element window (> 256 registers)
+        if constexpr (FIRST) {
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            r64::step8(d + i, 8);
-            __builtin_amdgcn_sched_barrier(0);
+            for (int i = 0; i < 8; i++) {
+                r64::step8(d + i, 8);
+                if ((i + 1) % IL == 0) __builtin_amdgcn_sched_barrier(0);
+            }
         }
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             r64::step8(d + 8 * i, 1);
-            __builtin_amdgcn_sched_barrier(0);
+            if ((i + 1) % IL == 0) __builtin_amdgcn_sched_barrier(0);
         }
     } else {
 #pragma unroll
@@ -722,6 +728,7 @@ constexpr unsigned kFixDirect = N == 16 ? 32u : 128u;
 #define DCTE_FIX_PIPE 1  // sparse strips (N = 8, 16): dword row fetches, next window in flight
 #endif
 
+
 template <int N, int SEM>
 struct FixStrip {
     static constexpr int LW = 64 + N - 1;             // luma columns of a strip
@@ -776,12 +783,18 @@ __device__ __forceinline__ void refine_group(const double* lum, int LW, int at, 
                       w, l, best, edge);
 }
 
+#ifndef DCTE_FIX_LANES
+#define DCTE_FIX_LANES 1 // dense strips at N = 8: one lane per pixel, window in registers
+#endif
 // grey layers at N <= 8 fit 128 VGPRs: 4 waves per SIMD (the LDS allows them)
 #ifndef DCTE_FIX_MINW
 #define DCTE_FIX_MINW 4
 #endif
+#ifndef DCTE_FIX_MINW_LANES
+#define DCTE_FIX_MINW_LANES 2   // N = 8 with lane-per-pixel dense strips: the window alone is 128 VGPRs
+#endif
 template <int N, int BPP>
-constexpr int kFixMinWaves = (BPP == 1 && N <= 8) ? DCTE_FIX_MINW : 1;
+constexpr int kFixMinWaves = (BPP == 1 && N <= 8) ? ((N == 8 && DCTE_FIX_LANES) ? DCTE_FIX_MINW_LANES : DCTE_FIX_MINW) : 1;
 
 template <int N, int BPP, int SEM>
 __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(const TileFixParams tp)
@@ -1062,8 +1075,8 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
             }
         }
 
-        // the batch's dense strips, one at a time
-        uint64_t dense_mask = __ballot(!sparse && sl == 0);
+        // the batch's dense strips, one at a time (N = 8: dcte_fix_dense8)
+        uint64_t dense_mask = (N == 8 && DCTE_FIX_LANES) ? 0ull : __ballot(!sparse && sl == 0);
         while (dense_mask) {                                              // uniform
             const int leader = __builtin_ctzll(dense_mask);             // lane 0 of its group
             dense_mask &= dense_mask - 1;
@@ -1317,6 +1330,150 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
     }
 }
 
+// Dense strips at N = 8 (more than kFixDirect<8> flagged pixels; the sparse
+// ones stay with dcte_fix_strips): one lane per flagged pixel, its whole
+// window in registers.  The eight window rows come straight from the frame as
+// whole dwords (neighbouring windows share rows: L1 / L2 hits), each byte is
+// converted through the LDS tables, and refine_regs runs both passes of
+// ddct8x8s and the last-maximum scan with no LDS round trip and no cross-lane
+// step -- eight independent 8-point transforms per pass keep the lane busy
+// where the group-per-window form of dcte_fix_strips waited on LDS transposes
+// (line art RGB at 16384^2: 1.27 -> 0.46 ms, profiles/r03/fix_lanes_ab.jsonl).
+// A kernel of its own: no band staging, so only the tables take LDS and the
+// register count sets the occupancy.  Waves take dirty strips in turn.
+#ifndef DCTE_DENSE8_MINW
+#define DCTE_DENSE8_MINW 2
+#endif
+#ifndef DCTE_DENSE8_RB
+#define DCTE_DENSE8_RB 8      // window rows per load batch
+#endif
+#ifndef DCTE_DENSE8_FUSE
+#define DCTE_DENSE8_FUSE 0    // liblqr: first-pass step of each row as soon as it is converted
+#endif
+template <int BPP, int SEM>
+__global__ __launch_bounds__(64, DCTE_DENSE8_MINW) void dcte_fix_dense8(const TileFixParams tp)
+{
+    constexpr int N = 8;
+    constexpr int HL = Geo<N, SEM>::HL;
+    constexpr bool kTab = SEM == kSemLqr && BPP == 3;
+    __shared__ double lut[kTab ? 3 * 256 : 256];
+    const MapParams& p = tp.m;
+    const unsigned ndirty = *p.dirty_count;
+    if (blockIdx.x >= ndirty) return;                  // uniform
+    const int lane = threadIdx.x;
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const int v = lane + 64 * t;
+        const double q = (double)v / 255;
+        if constexpr (kTab) {
+            lut[v] = 0.2126 * q;
+            lut[256 + v] = 0.7152 * q;
+            lut[512 + v] = 0.0722 * q;
+        } else {
+            lut[v] = q;
+        }
+    }
+    wave_sync_lds();
+    const uintptr_t pbase = reinterpret_cast<uintptr_t>(p.px);
+    const uint32_t base_off = (uint32_t)(pbase & 3u);
+    const unsigned nrec = base_off + (unsigned)((long long)(p.in_rows - 1) * p.rowstride) +
+                          (unsigned)(p.w * BPP);
+    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(pbase - base_off), (short)0, (int)nrec, (int)kBufFlags);
+    // liblqr luma (src/render.c:315, LQR_ER_LUMA) [liblqr, unverified] in the
+    // reference's order ((k_r r + k_g g) + k_b b); preview: RGB2LUMINANCE
+    auto luma3 = [&](uint32_t c0, uint32_t c1, uint32_t c2) -> double {
+        if constexpr (SEM == kSemLqr) {
+            if constexpr (BPP == 1) return lut[c0];
+            else return lut[c0] + lut[256 + c1] + lut[512 + c2];
+        } else {
+            return (double)preview_luma(c0, c1, c2, BPP);
+        }
+    };
+    const unsigned spt = (unsigned)tp.tile_w / 64u;   // strips per map tile
+    constexpr int NW = (8 * BPP + 3) / 4 + 1;         // dwords of a row's 8 pixels, any alignment
+    for (unsigned k = blockIdx.x; k < ndirty; k += gridDim.x) {   // uniform
+        const unsigned strip = p.dirty_list[k];
+        const unsigned cnt = p.tile_count[strip];
+        if (cnt <= kFixDirect<N>) continue;            // sparse: dcte_fix_strips
+        const unsigned tile = strip / spt;
+        const int bx = (int)(tile % (unsigned)tp.tiles_x), by = (int)(tile / (unsigned)tp.tiles_x);
+        const int sx0 = bx * tp.tile_w + 64 * (int)(strip % spt);
+        const int ys = p.y0 + by * p.tile_h;
+        const unsigned* list = p.fix_list + (size_t)strip * (size_t)(64 * p.tile_h);
+        for (unsigned q0 = 0; q0 < cnt; q0 += 64) {   // uniform
+            const unsigned q = q0 + (unsigned)lane;
+            if (q >= cnt) continue;
+            const unsigned loc = list[q];
+            const int lx = (int)(loc & 63), ly = (int)(loc >> 6);
+            const int x = sx0 + lx, y = ys + ly;
+            const int gx0 = x - HL;
+            const bool inside = gx0 >= 0 && gx0 + 8 <= p.w;
+            // rows in batches of RB: a batch's loads are issued, then its
+            // bytes converted (liblqr: each row's first-pass step right away
+            // -- the reference's first pass runs along x for each window row,
+            // src/fft2d/shrtdct.c:62-89, so it needs that row alone)
+            constexpr int RB = DCTE_DENSE8_RB;
+            double d[64];
+#pragma unroll
+            for (int r0 = 0; r0 < 8; r0 += RB) {
+                uint32_t fv[RB][NW];
+                uint32_t foff[RB];
+                bool fast[RB];
+#pragma unroll
+                for (int rr = 0; rr < RB; rr++) {
+                    const int gy = clampi(y - HL + r0 + rr, 0, p.h - 1);
+                    const uint32_t s0 = base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
+                                        (uint32_t)(gx0 * BPP);
+                    fast[rr] = inside && ((s0 + 8 * BPP - 1) | 3u) < nrec;
+                    foff[rr] = s0 & 3u;
+                    const uint32_t a = fast[rr] ? (s0 & ~3u) : 0x7ffffff0u;   // past num_records: zeros
+#pragma unroll
+                    for (int j = 0; j < NW; j++)
+                        fv[rr][j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * j), 0, 0);
+                }
+#pragma unroll
+                for (int rr = 0; rr < RB; rr++) {
+                    const int r = r0 + rr;
+                    double lv[8];
+                    if (fast[rr]) {
+                        uint32_t wd[NW - 1];
+#pragma unroll
+                        for (int j = 0; j < NW - 1; j++)
+                            wd[j] = __builtin_amdgcn_alignbyte(fv[rr][j + 1], fv[rr][j], foff[rr]);
+#pragma unroll
+                        for (int c = 0; c < 8; c++) {
+                            auto byte = [&](int b) { return (wd[b >> 2] >> (8 * (b & 3))) & 255u; };
+                            lv[c] = luma3(byte(c * BPP), BPP > 1 ? byte(c * BPP + 1) : 0u,
+                                          BPP > 1 ? byte(c * BPP + 2) : 0u);
+                        }
+                    } else {
+                        // clamped at the left / right frame border, or at the
+                        // frame's last bytes: per-pixel reads
+                        const int gy = clampi(y - HL + r, 0, p.h - 1);
+                        const uint8_t* row = p.px + (long long)(gy - p.in_row0) * p.rowstride;
+#pragma unroll
+                        for (int c = 0; c < 8; c++) {
+                            const uint8_t* q8 = row + (long long)clampi(gx0 + c, 0, p.w - 1) * BPP;
+                            lv[c] = luma3(q8[0], BPP > 1 ? q8[1] : 0u, BPP > 1 ? q8[2] : 0u);
+                        }
+                    }
+                    if constexpr (SEM == kSemLqr && DCTE_DENSE8_FUSE) r64::step8(lv, 1);
+                    // image row r, pixel c: liblqr data[c][r], preview data[r][c]
+#pragma unroll
+                    for (int c = 0; c < 8; c++) d[SEM == kSemLqr ? c * 8 + r : r * 8 + c] = lv[c];
+                }
+            }
+            double m;
+            bool edge;
+            if constexpr (SEM == kSemLqr && DCTE_DENSE8_FUSE) refine_regs<8, DCTE_FIX_IL, false>(d, tp.ct, m, edge);
+            else refine_regs<8>(d, tp.ct, m, edge);
+            p.out[(long long)(y - p.y0) * p.out_stride + x] =
+                edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
+        }
+    }
+}
+
 // ------------------------------------------------------------------ windows
 // dctNxN + weighted_max_dct_correlation (src/dct.c:77-110) on windows the
 // caller filled -- the per-window form of the callback (src/render.c:146-155
@@ -1461,6 +1618,25 @@ static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
     }
     const int blocks = nstrips < resident ? nstrips : resident;
     hipLaunchKernelGGL((dcte_fix_strips<N, BPP, SEM>), dim3(blocks), dim3(64), 0, s, p);
+    if constexpr (N == 8 && DCTE_FIX_LANES) {
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        static std::atomic<int> dcache[kMaxDevices];
+        int dres = dev >= 0 && dev < kMaxDevices ? dcache[dev].load(std::memory_order_relaxed) : 0;
+        if (!dres) {
+            int cus = 0, per_cu = 0;
+            if (dev >= 0 &&
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dcte_fix_dense8<BPP, SEM>, 64, 0) ==
+                    hipSuccess && cus > 0 && per_cu > 0)
+                dres = cus * per_cu;
+            else
+                dres = 2048;
+            if (dev >= 0 && dev < kMaxDevices) dcache[dev].store(dres, std::memory_order_relaxed);
+        }
+        const int dblocks = nstrips < dres ? nstrips : dres;
+        hipLaunchKernelGGL((dcte_fix_dense8<BPP, SEM>), dim3(dblocks), dim3(64), 0, s, p);
+    }
     return hipGetLastError();
 }
 

@@ -49,7 +49,9 @@ EXPORTS = ("dcte_abi_version", "dcte_device_count", "dcte_create", "dcte_destroy
            "dcte_normalize_u8_device", "dcte_seam_carve_device", "dcte_energy_points",
            "dcte_energy_points_device", "dcte_seam_find_device", "dcte_seam_find",
            "dcte_carve", "dcte_energy_windows", "dcte_energy_windows_device",
-           "dcte_energy_window", "dcte_normalize_u8_host")
+           "dcte_energy_window", "dcte_normalize_u8_host", "dcte_carver_create",
+           "dcte_carver_step", "dcte_carver_width", "dcte_carver_height",
+           "dcte_carver_band_width", "dcte_carver_destroy")
 
 _lib = None
 
@@ -151,6 +153,16 @@ def lib():
     L.dcte_energy_window.argtypes = [i, vp, f, f, vp]
     L.dcte_normalize_u8_host.restype = i
     L.dcte_normalize_u8_host.argtypes = [vp, ctypes.c_size_t, i, i, vp]
+    L.dcte_carver_create.restype = i
+    L.dcte_carver_create.argtypes = [vp, vp, i, i, i, ctypes.c_size_t, i, f, f, i, vp,
+                                     ctypes.POINTER(vp)]
+    L.dcte_carver_step.restype = i
+    L.dcte_carver_step.argtypes = [vp, vp, vp, vp, vp]
+    for fn in ("dcte_carver_width", "dcte_carver_height", "dcte_carver_band_width"):
+        getattr(L, fn).restype = i
+        getattr(L, fn).argtypes = [vp]
+    L.dcte_carver_destroy.restype = None
+    L.dcte_carver_destroy.argtypes = [vp]
     L.dcte_strerror.restype = ctypes.c_char_p
     L.dcte_strerror.argtypes = [ctypes.c_int]
     L.dcte_last_error.restype = ctypes.c_char_p
@@ -414,6 +426,19 @@ class Context:
                                               edges, textures, out.ctypes.data))
         return out
 
+    # -- device mirror of a liblqr carver (the update_emap hook)
+    def carver(self, px, n=8, edges=0.5, textures=0.5, transposed=False):
+        """-> (Carver, first map of the mirrored frame)."""
+        px = np.ascontiguousarray(px, dtype=np.uint8)
+        h, w = px.shape[:2]
+        bpp = 1 if px.ndim == 2 else px.shape[2]
+        first = np.empty((w, h) if transposed else (h, w), np.float32)
+        c = ctypes.c_void_p()
+        self._check(lib().dcte_carver_create(self._h, px.ctypes.data, w, h, bpp, _rowstride(px), n,
+                                             edges, textures, int(bool(transposed)),
+                                             first.ctypes.data, ctypes.byref(c)))
+        return Carver(self, c, bpp), first
+
     # -- minimum-energy seam (SURVEY §8f-4)
     def seam_find(self, E):
         """Vertical seam (column per row) of an HxW float32 host energy map."""
@@ -462,7 +487,48 @@ class Context:
         return seam
 
 
-__all__ = ["Context", "DcteError", "lib", "device_count", "LIB_PATH", "EXPORTS",
+class Carver:
+    """dcte_carver: the carver's frame and map in HBM; step() carves the seam
+    liblqr's DP picks and returns (seam, band_x0, band energies, band pixels)."""
+
+    def __init__(self, ctx, handle, bpp):
+        self._ctx, self._h, self.bpp = ctx, handle, bpp
+
+    @property
+    def width(self):
+        return lib().dcte_carver_width(self._h)
+
+    @property
+    def height(self):
+        return lib().dcte_carver_height(self._h)
+
+    @property
+    def band_width(self):
+        return lib().dcte_carver_band_width(self._h)
+
+    def step(self):
+        H, bw = self.height, self.band_width
+        seam = np.empty(H, np.int32)
+        x0 = np.empty(H, np.int32)
+        e = np.empty((H, bw), np.float32)
+        px = np.empty((H, bw, self.bpp), np.uint8)
+        self._ctx._check(lib().dcte_carver_step(self._h, seam.ctypes.data, x0.ctypes.data,
+                                                e.ctypes.data, px.ctypes.data))
+        return seam, x0, e, px
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().dcte_carver_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+__all__ = ["Context", "Carver", "DcteError", "lib", "device_count", "LIB_PATH", "EXPORTS",
            "energy_window", "normalize_u8_host",
            "DCTE_LQR", "DCTE_PREVIEW", "DCTE_OPT_TIE_TAU", "DCTE_OPT_PROFILE", "DCTE_OPT_PIN_HOST", "DCTE_OPT_TILE_H", "DCTE_OPT_DP_BANDWISE", "DCTE_OPT_DP_SPIN_LIMIT",
            "DCTE_NORM_LQR", "DCTE_NORM_PREVIEW"]

@@ -181,3 +181,32 @@ def test_gpu_map_serves_transposed_carver(n):
     assert calls == 0
     ref = O.energy_map(np.ascontiguousarray(np.swapaxes(img, 0, 1)), n, 0.15, 0.85)
     assert within_tol(out, ref).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,transposed", [(8, False), (8, True), (16, False), (4, True)])
+def test_carver_mirror_band_is_the_map_of_the_carved_frame(n, transposed):
+    """dcte_carver (the hook's device mirror): its first map is dcte_energy_map
+    of the (transposed) frame; each step removes the seam dcte_seam_find picks
+    on the current map, and the band it returns holds exactly the pixels and
+    the dcte_energy_map energies of the carved frame at those columns."""
+    img = load_input("natural_rgb_97x41.npy")
+    px = np.ascontiguousarray(np.swapaxes(img, 0, 1)) if transposed else img.copy()
+    with dctenergy.Context(ngpus=1) as ctx:
+        c, first = ctx.carver(img, n, 0.3, 0.7, transposed)
+        assert np.array_equal(first, ctx.energy_map(px, n, 0.3, 0.7))
+        H = px.shape[0]
+        assert c.height == H and c.width == px.shape[1] and c.band_width == 2 * n + 4
+        for _ in range(6):
+            want = ctx.seam_find(ctx.energy_map(px, n, 0.3, 0.7))
+            seam, x0, e, bpx = c.step()
+            assert np.array_equal(seam, want)
+            px = np.ascontiguousarray(np.stack([np.delete(px[y], seam[y], axis=0) for y in range(H)]))
+            E = ctx.energy_map(px, n, 0.3, 0.7)
+            W = px.shape[1]
+            assert c.width == W
+            for y in range(H):
+                cols = np.minimum(x0[y] + np.arange(c.band_width), W - 1)
+                assert np.array_equal(e[y], E[y, cols])
+                assert np.array_equal(bpx[y], px[y, cols])
+        c.close()
