@@ -76,6 +76,9 @@ namespace dcte {
 #ifndef DCTE_XBAL
 #define DCTE_XBAL 1        // halo-column luma conversions spread one per lane of the last wave
 #endif
+#ifndef DCTE_DIRECT
+#define DCTE_DIRECT 1      // N = 8: each lane loads its own pixel's bytes (dwordx2), no raw LDS stage (-1.8 %)
+#endif
 constexpr unsigned kBufFlags = 0x00020000u;  // gfx9 raw buffer dword3
 
 // SEM = kSemLqr    : liblqr callback window, offsets -(N/2-1)..N/2
@@ -144,7 +147,10 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
     // (N = 16 keeps one buffer: its LDS combine of partial maxima adds one anyway)
     constexpr bool kDB = DCTE_DB && S == 1;
     constexpr int NB = kDB ? 2 : 1;
-    __shared__ uint32_t raw[NB][G][NDW];
+    // DCTE_DIRECT (below) needs no raw stage
+    constexpr bool kDirectLds = DCTE_DIRECT && S == 1 && kDB && !(N <= DCTE_PF2_MAXN) &&
+                                LW - kThreads > 0 && (LW - kThreads) * G <= 64;
+    __shared__ uint32_t raw[kDirectLds ? 1 : NB][kDirectLds ? 1 : G][kDirectLds ? 1 : NDW];
     __shared__ float lum[NB][G][LWP];
     // S = 4 (N = 16): per-wave partial maxima of the group's rows; only the
     // waves owning k1 = 0 (q = 0) and k1 = 1 (q = 2) carry an edge candidate
@@ -222,6 +228,77 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
             for (int q = 0; q < DPT; q++) {
                 const int dw = tx + q * kThreads;
                 pref[PB][u][q] = (dw < NDW) ? __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * dw), 0, 0) : 0u;
+            }
+        }
+    };
+
+    // DCTE_DIRECT: no raw stage in LDS.  Each lane fetches the bytes of its
+    // own column of each row of a group with one 8-byte buffer load (any
+    // alignment: the pixel's <= 4 bytes lie inside it), one group ahead, and
+    // converts them straight from registers; the last wave's lanes also fetch
+    // the N - 1 halo columns' pixels (one (row, column) each, as DCTE_XBAL).
+    // The convert phase then waits on no LDS reads.
+    constexpr int XH = LW - kThreads;                  // halo columns past one per lane
+    constexpr bool kDirect = DCTE_DIRECT && S == 1 && kDB && PFD == 1 && XH > 0 && XH * G <= 64;
+    static_assert(kDirect == kDirectLds, "raw stage sizing");
+    uint32_t dlo[kDirect ? G : 1], dhi[kDirect ? G : 1];
+    uint32_t xlo = 0, xhi = 0;
+    const int hlane = tx - (kThreads - 64);
+    const bool has_halo = kDirect && hlane >= 0 && hlane < XH * G;
+    const int hrow = has_halo ? hlane / XH : 0, hcc = has_halo ? kThreads + hlane % XH : 0;
+    auto col_bytes = [&](int cc) -> uint32_t {         // byte offset of column cc from xs
+        return (uint32_t)((clampi(x0 - HL + cc, 0, w - 1) - xs) * BPP);
+    };
+    auto fetch2 = [&](uint32_t a) __attribute__((always_inline)) {
+        const uint32_t a4 = a & ~3u;
+        auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)a4, 0, 0);
+        if (tail_wg) {                                  // uniform; a handful of WGs
+            if (a4 == nrec4) v[0] = tail;
+            else if (a4 + 4u == nrec4) v[1] = tail;
+        }
+        return v;
+    };
+    auto issue_direct = [&](int g) __attribute__((always_inline)) {
+        if constexpr (kDirect) {
+#pragma unroll
+            for (int u = 0; u < G; u++) {
+                const int i = g * G + u;
+                const auto v = fetch2(row_start(i < n_in ? i : n_in - 1) + col_bytes(tx));
+                dlo[u] = v[0];
+                dhi[u] = v[1];
+            }
+            if (has_halo) {
+                const int i = g * G + hrow;
+                const auto v = fetch2(row_start(i < n_in ? i : n_in - 1) + col_bytes(hcc));
+                xlo = v[0];
+                xhi = v[1];
+            }
+        }
+    };
+    auto luma_bytes = [&](uint32_t wd) -> float {       // exact integer luma (biased) of a pixel's bytes
+        const uint32_t c0 = wd & 255u, c1 = BPP >= 3 ? (wd >> 8) & 255u : 0u, c2 = BPP >= 3 ? (wd >> 16) & 255u : 0u;
+        int L;
+        if constexpr (SEM == kSemLqr) {
+            L = (BPP == 1) ? kLumaGrey * (int)c0
+                           : kLumaR * (int)c0 + kLumaG * (int)c1 + kLumaB * (int)c2;
+            L -= kLumaBias;
+        } else {
+            L = (int)preview_luma(c0, c1, c2, BPP) - kPreviewBias;
+        }
+        return (float)L;
+    };
+    auto convert_direct = [&](int g, int b) __attribute__((always_inline)) {
+        if constexpr (kDirect) {
+#pragma unroll
+            for (int u = 0; u < G; u++) {
+                const int i = g * G + u;
+                const uint32_t off = (row_start(i < n_in ? i : n_in - 1) + col_bytes(tx)) & 3u;
+                lum[b][u][tx] = luma_bytes(__builtin_amdgcn_alignbyte(dhi[u], dlo[u], off));
+            }
+            if (has_halo) {
+                const int i = g * G + hrow;
+                const uint32_t off = (row_start(i < n_in ? i : n_in - 1) + col_bytes(hcc)) & 3u;
+                lum[b][hrow][hcc] = luma_bytes(__builtin_amdgcn_alignbyte(xhi, xlo, off));
             }
         }
     };
@@ -391,7 +468,7 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
         else __builtin_amdgcn_s_setprio(0);
     };
     constexpr std::integral_constant<int, 0> P0{};
-    issue(0, P0);
+    if constexpr (!kDirect) issue(0, P0);
     if constexpr (kDB && PFD == 2) {
         // As below, with groups g + 2 AND g + 3 in flight while group g is
         // computed: the group staged next comes from pref[(g + 1) & 1], which
@@ -421,6 +498,24 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
             step(g, 0, P1);
             if (g + 1 >= ngroups) break;
             step(g + 1, 1, P0);
+        }
+    } else if constexpr (kDirect) {
+        // As below without the raw stage: group g's bytes are in registers
+        // (loaded during group g - 1's passes), converted into lum[b], then
+        // group g + 1's loads go out; one barrier; group g's passes.
+        issue_direct(0);
+        for (int g = 0; g < ngroups; g++) {
+            const int b = g & 1;
+#if DCTE_PRIO
+            set_prio(true, g);
+#endif
+            convert_direct(g, b);
+            if (g + 1 < ngroups) issue_direct(g + 1);
+            __syncthreads();
+#if DCTE_PRIO
+            set_prio(false, g);
+#endif
+            compute(g, b);
         }
     } else if constexpr (kDB) {
         // One barrier per group: group g is converted and group g + 1 staged
@@ -618,6 +713,45 @@ __device__ __forceinline__ void refine_regs(double (&d)[N * N], const double* ct
 #pragma unroll
     for (int e = N + 1; e < N * N; e++) ma = fmax(ma, fabs(d[e]));
     lastmax_decide(fabs(d[1]), fabs(d[N]), mb, ma, m, edge);
+}
+
+// N = 8, first pass done: the second pass and the last-maximum scan, with
+// columns that cannot hold the maximum skipped.  The second pass is
+// orthonormal (ddct8x8s, src/fft2d/shrtdct.c:90-117), so every output of
+// coefficient row k1 is at most the row's norm ||F[k1][.]|| (up to ~1e-15
+// relative rounding): once rows 0 and 1 (the two edge atoms) are transformed,
+// a row whose squared norm, with a 1e-12 relative margin, is below the square
+// of the running maximum can neither be the maximum nor tie it, and the
+// last-maximum scan (lastmax_decide) never looks at it.  The skip is taken
+// only when no lane of the wave needs the row (lane-per-pixel path).
+__device__ __forceinline__ void refine8_second_skip(double (&d)[64], double& m, bool& edge)
+{
+    r64::step8(d, 1);
+    r64::step8(d + 8, 1);
+    const double a01 = fabs(d[1]), a10 = fabs(d[8]);
+    double mb = -1.0, ma = -1.0;
+#pragma unroll
+    for (int e = 2; e < 8; e++) mb = fmax(mb, fabs(d[e]));
+#pragma unroll
+    for (int e = 9; e < 16; e++) ma = fmax(ma, fabs(d[e]));
+    double run = fmax(fmax(a01, a10), fmax(mb, ma));
+#pragma unroll
+    for (int k = 2; k < 8; k++) {
+        double n2 = 0.0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) n2 = fma(d[8 * k + j], d[8 * k + j], n2);
+        const bool need = n2 * (1.0 + 1e-12) >= run * run * (1.0 - 1e-12);
+        if (__any(need)) {                            // uniform
+            r64::step8(d + 8 * k, 1);
+            double cm = -1.0;
+#pragma unroll
+            for (int j = 0; j < 8; j++) cm = fmax(cm, fabs(d[8 * k + j]));
+            ma = fmax(ma, cm);
+            run = fmax(run, cm);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    lastmax_decide(a01, a10, mb, ma, m, edge);
 }
 
 __device__ __forceinline__ void wave_sync_lds()
@@ -1350,6 +1484,9 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
 #ifndef DCTE_DENSE8_FUSE
 #define DCTE_DENSE8_FUSE 0    // liblqr: first-pass step of each row as soon as it is converted
 #endif
+#ifndef DCTE_DENSE8_SKIP
+#define DCTE_DENSE8_SKIP 0    // skip second-pass rows whose norm is below the running maximum
+#endif
 template <int BPP, int SEM>
 __global__ __launch_bounds__(64, DCTE_DENSE8_MINW) void dcte_fix_dense8(const TileFixParams tp)
 {
@@ -1466,8 +1603,20 @@ __global__ __launch_bounds__(64, DCTE_DENSE8_MINW) void dcte_fix_dense8(const Ti
             }
             double m;
             bool edge;
-            if constexpr (SEM == kSemLqr && DCTE_DENSE8_FUSE) refine_regs<8, DCTE_FIX_IL, false>(d, tp.ct, m, edge);
-            else refine_regs<8>(d, tp.ct, m, edge);
+            if constexpr (DCTE_DENSE8_SKIP) {
+                if constexpr (!(SEM == kSemLqr && DCTE_DENSE8_FUSE)) {
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        r64::step8(d + i, 8);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
+                refine8_second_skip(d, m, edge);
+            } else if constexpr (SEM == kSemLqr && DCTE_DENSE8_FUSE) {
+                refine_regs<8, DCTE_FIX_IL, false>(d, tp.ct, m, edge);
+            } else {
+                refine_regs<8>(d, tp.ct, m, edge);
+            }
             p.out[(long long)(y - p.y0) * p.out_stride + x] =
                 edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
         }
