@@ -49,6 +49,7 @@ struct TileFixParams {
     unsigned* fix_total;     // += pixels refined (host-path diagnostic), or null
     int tiles_x;             // map grid width in tiles
     int tile_w;              // map tile width in columns (map_tile_w)
+    int sparse_blocks;       // N = 8: blocks of the launch that walk sparse strips (the rest: dense)
 };
 
 struct FixParams {

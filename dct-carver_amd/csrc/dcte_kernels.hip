@@ -920,6 +920,9 @@ __device__ __forceinline__ void refine_group(const double* lum, int LW, int at, 
 #ifndef DCTE_FIX_LANES
 #define DCTE_FIX_LANES 1 // dense strips at N = 8: one lane per pixel, window in registers
 #endif
+#ifndef DCTE_FIX_MERGE
+#define DCTE_FIX_MERGE 1 // ... run by extra blocks of the dcte_fix_strips launch (one launch less)
+#endif
 // grey layers at N <= 8 fit 128 VGPRs: 4 waves per SIMD (the LDS allows them)
 #ifndef DCTE_FIX_MINW
 #define DCTE_FIX_MINW 4
@@ -929,6 +932,182 @@ __device__ __forceinline__ void refine_group(const double* lum, int LW, int at, 
 #endif
 template <int N, int BPP>
 constexpr int kFixMinWaves = (BPP == 1 && N <= 8) ? ((N == 8 && DCTE_FIX_LANES) ? DCTE_FIX_MINW_LANES : DCTE_FIX_MINW) : 1;
+
+// Dense strips at N = 8 (more than kFixDirect<8> flagged pixels; the sparse
+// ones stay with dcte_fix_strips): one lane per flagged pixel, its whole
+// window in registers.  The eight window rows come straight from the frame as
+// whole dwords (neighbouring windows share rows: L1 / L2 hits), each byte is
+// converted through the LDS tables, and refine_regs runs both passes of
+// ddct8x8s and the last-maximum scan with no LDS round trip and no cross-lane
+// step -- eight independent 8-point transforms per pass keep the lane busy
+// where the group-per-window form of dcte_fix_strips waited on LDS transposes
+// (line art RGB at 16384^2: 1.27 -> 0.46 ms, profiles/r03/fix_lanes_ab.jsonl).
+// A kernel of its own: no band staging, so only the tables take LDS and the
+// register count sets the occupancy.  Waves take dirty strips in turn.
+#ifndef DCTE_DENSE8_MINW
+#define DCTE_DENSE8_MINW 2
+#endif
+#ifndef DCTE_DENSE8_RB
+#define DCTE_DENSE8_RB 8      // window rows per load batch
+#endif
+#ifndef DCTE_DENSE8_FUSE
+#define DCTE_DENSE8_FUSE 0    // liblqr: first-pass step of each row as soon as it is converted
+#endif
+#ifndef DCTE_DENSE8_SKIP
+#define DCTE_DENSE8_SKIP 0    // skip second-pass rows whose norm is below the running maximum
+#endif
+// the 256 liblqr channel quotients v / 255 (pre-weighted per channel for
+// liblqr RGB: kTab), as the reference divides (bit-identical)
+template <bool kTab>
+__device__ __forceinline__ void fill_luma_lut(double* lut, int lane)
+{
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const int v = lane + 64 * t;
+        const double q = (double)v / 255;
+        if constexpr (kTab) {
+            lut[v] = 0.2126 * q;
+            lut[256 + v] = 0.7152 * q;
+            lut[512 + v] = 0.0722 * q;
+        } else {
+            lut[v] = q;
+        }
+    }
+}
+
+// The dense-strip walk of one wave: wave `blk` of `nblk` takes dirty strips
+// blk, blk + nblk, ...; `lut` filled by fill_luma_lut.
+template <int BPP, int SEM>
+__device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const double* lut,
+                                               unsigned blk, unsigned nblk)
+{
+    constexpr int N = 8;
+    constexpr int HL = Geo<N, SEM>::HL;
+    const MapParams& p = tp.m;
+    const unsigned ndirty = *p.dirty_count;
+    const int lane = threadIdx.x;
+    const uintptr_t pbase = reinterpret_cast<uintptr_t>(p.px);
+    const uint32_t base_off = (uint32_t)(pbase & 3u);
+    const unsigned nrec = base_off + (unsigned)((long long)(p.in_rows - 1) * p.rowstride) +
+                          (unsigned)(p.w * BPP);
+    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(pbase - base_off), (short)0, (int)nrec, (int)kBufFlags);
+    // liblqr luma (src/render.c:315, LQR_ER_LUMA) [liblqr, unverified] in the
+    // reference's order ((k_r r + k_g g) + k_b b); preview: RGB2LUMINANCE
+    auto luma3 = [&](uint32_t c0, uint32_t c1, uint32_t c2) -> double {
+        if constexpr (SEM == kSemLqr) {
+            if constexpr (BPP == 1) return lut[c0];
+            else return lut[c0] + lut[256 + c1] + lut[512 + c2];
+        } else {
+            return (double)preview_luma(c0, c1, c2, BPP);
+        }
+    };
+    const unsigned spt = (unsigned)tp.tile_w / 64u;   // strips per map tile
+    constexpr int NW = (8 * BPP + 3) / 4 + 1;         // dwords of a row's 8 pixels, any alignment
+    for (unsigned k = blk; k < ndirty; k += nblk) {   // uniform
+        const unsigned strip = p.dirty_list[k];
+        const unsigned cnt = p.tile_count[strip];
+        if (cnt <= kFixDirect<N>) continue;            // sparse: dcte_fix_strips
+        const unsigned tile = strip / spt;
+        const int bx = (int)(tile % (unsigned)tp.tiles_x), by = (int)(tile / (unsigned)tp.tiles_x);
+        const int sx0 = bx * tp.tile_w + 64 * (int)(strip % spt);
+        const int ys = p.y0 + by * p.tile_h;
+        const unsigned* list = p.fix_list + (size_t)strip * (size_t)(64 * p.tile_h);
+        for (unsigned q0 = 0; q0 < cnt; q0 += 64) {   // uniform
+            const unsigned q = q0 + (unsigned)lane;
+            if (q >= cnt) continue;
+            const unsigned loc = list[q];
+            const int lx = (int)(loc & 63), ly = (int)(loc >> 6);
+            const int x = sx0 + lx, y = ys + ly;
+            const int gx0 = x - HL;
+            const bool inside = gx0 >= 0 && gx0 + 8 <= p.w;
+            // rows in batches of RB: a batch's loads are issued, then its
+            // bytes converted (liblqr: each row's first-pass step right away
+            // -- the reference's first pass runs along x for each window row,
+            // src/fft2d/shrtdct.c:62-89, so it needs that row alone)
+            constexpr int RB = DCTE_DENSE8_RB;
+            double d[64];
+#pragma unroll
+            for (int r0 = 0; r0 < 8; r0 += RB) {
+                uint32_t fv[RB][NW];
+                uint32_t foff[RB];
+                bool fast[RB];
+#pragma unroll
+                for (int rr = 0; rr < RB; rr++) {
+                    const int gy = clampi(y - HL + r0 + rr, 0, p.h - 1);
+                    const uint32_t s0 = base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
+                                        (uint32_t)(gx0 * BPP);
+                    fast[rr] = inside && ((s0 + 8 * BPP - 1) | 3u) < nrec;
+                    foff[rr] = s0 & 3u;
+                    const uint32_t a = fast[rr] ? (s0 & ~3u) : 0x7ffffff0u;   // past num_records: zeros
+#pragma unroll
+                    for (int j = 0; j < NW; j++)
+                        fv[rr][j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * j), 0, 0);
+                }
+#pragma unroll
+                for (int rr = 0; rr < RB; rr++) {
+                    const int r = r0 + rr;
+                    double lv[8];
+                    if (fast[rr]) {
+                        uint32_t wd[NW - 1];
+#pragma unroll
+                        for (int j = 0; j < NW - 1; j++)
+                            wd[j] = __builtin_amdgcn_alignbyte(fv[rr][j + 1], fv[rr][j], foff[rr]);
+#pragma unroll
+                        for (int c = 0; c < 8; c++) {
+                            auto byte = [&](int b) { return (wd[b >> 2] >> (8 * (b & 3))) & 255u; };
+                            lv[c] = luma3(byte(c * BPP), BPP > 1 ? byte(c * BPP + 1) : 0u,
+                                          BPP > 1 ? byte(c * BPP + 2) : 0u);
+                        }
+                    } else {
+                        // clamped at the left / right frame border, or at the
+                        // frame's last bytes: per-pixel reads
+                        const int gy = clampi(y - HL + r, 0, p.h - 1);
+                        const uint8_t* row = p.px + (long long)(gy - p.in_row0) * p.rowstride;
+#pragma unroll
+                        for (int c = 0; c < 8; c++) {
+                            const uint8_t* q8 = row + (long long)clampi(gx0 + c, 0, p.w - 1) * BPP;
+                            lv[c] = luma3(q8[0], BPP > 1 ? q8[1] : 0u, BPP > 1 ? q8[2] : 0u);
+                        }
+                    }
+                    if constexpr (SEM == kSemLqr && DCTE_DENSE8_FUSE) r64::step8(lv, 1);
+                    // image row r, pixel c: liblqr data[c][r], preview data[r][c]
+#pragma unroll
+                    for (int c = 0; c < 8; c++) d[SEM == kSemLqr ? c * 8 + r : r * 8 + c] = lv[c];
+                }
+            }
+            double m;
+            bool edge;
+            if constexpr (DCTE_DENSE8_SKIP) {
+                if constexpr (!(SEM == kSemLqr && DCTE_DENSE8_FUSE)) {
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        r64::step8(d + i, 8);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
+                refine8_second_skip(d, m, edge);
+            } else if constexpr (SEM == kSemLqr && DCTE_DENSE8_FUSE) {
+                refine_regs<8, DCTE_FIX_IL, false>(d, tp.ct, m, edge);
+            } else {
+                refine_regs<8>(d, tp.ct, m, edge);
+            }
+            p.out[(long long)(y - p.y0) * p.out_stride + x] =
+                edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
+        }
+    }
+}
+
+template <int BPP, int SEM>
+__global__ __launch_bounds__(64, DCTE_DENSE8_MINW) void dcte_fix_dense8(const TileFixParams tp)
+{
+    constexpr bool kTab = SEM == kSemLqr && BPP == 3;
+    __shared__ double lut[kTab ? 3 * 256 : 256];
+    if (blockIdx.x >= *tp.m.dirty_count) return;      // uniform
+    fill_luma_lut<kTab>(lut, threadIdx.x);
+    wave_sync_lds();
+    fix_dense8_run<BPP, SEM>(tp, lut, blockIdx.x, gridDim.x);
+}
 
 template <int N, int BPP, int SEM>
 __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(const TileFixParams tp)
@@ -970,13 +1149,25 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
     constexpr int WS = kGroup ? (N * (N + 1) + 7) / 8 * 8 + 8 : 1;
     // the band's raw rows and the groups' window buffers: one region when raw
     // is read only by the luma conversion (the windows only after it)
-    constexpr int RAW_D = (LR * PDW + 1) / 2, WIN_D = (kGroup ? PPW : 1) * WS;
+    // (N = 8 with dcte_fix_dense8 runs no dense band here: no raw band)
+    constexpr int RAW_D = (N == 8 && DCTE_FIX_LANES) ? 0 : (LR * PDW + 1) / 2, WIN_D = (kGroup ? PPW : 1) * WS;
     constexpr int RW_D = kOtf ? RAW_D + WIN_D : (RAW_D > WIN_D ? RAW_D : WIN_D);
     __shared__ __attribute__((aligned(16))) double rw_lds[RW_D];
     uint32_t* const raw = reinterpret_cast<uint32_t*>(rw_lds);
     double (*const win)[WS] = reinterpret_cast<double (*)[WS]>(rw_lds + (kOtf ? RAW_D : 0));
     const MapParams& p = tp.m;
     const unsigned ndirty = *p.dirty_count;
+    if constexpr (N == 8 && DCTE_FIX_LANES && DCTE_FIX_MERGE) {
+        // one launch for both: blocks past tp.sparse_blocks walk the dense strips
+        if (blockIdx.x >= (unsigned)tp.sparse_blocks) {
+            const unsigned blk = blockIdx.x - (unsigned)tp.sparse_blocks;
+            if (blk >= ndirty) return;                 // uniform
+            fill_luma_lut<kTab>(lut, threadIdx.x);
+            wave_sync_lds();
+            fix_dense8_run<BPP, SEM>(tp, lut, blk, gridDim.x - (unsigned)tp.sparse_blocks);
+            return;
+        }
+    }
     constexpr int SB = kGroup ? PPW : 8;               // strips per batch (below)
     if (blockIdx.x * SB >= ndirty) return;             // uniform
     const int lane = threadIdx.x;
@@ -1464,165 +1655,6 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
     }
 }
 
-// Dense strips at N = 8 (more than kFixDirect<8> flagged pixels; the sparse
-// ones stay with dcte_fix_strips): one lane per flagged pixel, its whole
-// window in registers.  The eight window rows come straight from the frame as
-// whole dwords (neighbouring windows share rows: L1 / L2 hits), each byte is
-// converted through the LDS tables, and refine_regs runs both passes of
-// ddct8x8s and the last-maximum scan with no LDS round trip and no cross-lane
-// step -- eight independent 8-point transforms per pass keep the lane busy
-// where the group-per-window form of dcte_fix_strips waited on LDS transposes
-// (line art RGB at 16384^2: 1.27 -> 0.46 ms, profiles/r03/fix_lanes_ab.jsonl).
-// A kernel of its own: no band staging, so only the tables take LDS and the
-// register count sets the occupancy.  Waves take dirty strips in turn.
-#ifndef DCTE_DENSE8_MINW
-#define DCTE_DENSE8_MINW 2
-#endif
-#ifndef DCTE_DENSE8_RB
-#define DCTE_DENSE8_RB 8      // window rows per load batch
-#endif
-#ifndef DCTE_DENSE8_FUSE
-#define DCTE_DENSE8_FUSE 0    // liblqr: first-pass step of each row as soon as it is converted
-#endif
-#ifndef DCTE_DENSE8_SKIP
-#define DCTE_DENSE8_SKIP 0    // skip second-pass rows whose norm is below the running maximum
-#endif
-template <int BPP, int SEM>
-__global__ __launch_bounds__(64, DCTE_DENSE8_MINW) void dcte_fix_dense8(const TileFixParams tp)
-{
-    constexpr int N = 8;
-    constexpr int HL = Geo<N, SEM>::HL;
-    constexpr bool kTab = SEM == kSemLqr && BPP == 3;
-    __shared__ double lut[kTab ? 3 * 256 : 256];
-    const MapParams& p = tp.m;
-    const unsigned ndirty = *p.dirty_count;
-    if (blockIdx.x >= ndirty) return;                  // uniform
-    const int lane = threadIdx.x;
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-        const int v = lane + 64 * t;
-        const double q = (double)v / 255;
-        if constexpr (kTab) {
-            lut[v] = 0.2126 * q;
-            lut[256 + v] = 0.7152 * q;
-            lut[512 + v] = 0.0722 * q;
-        } else {
-            lut[v] = q;
-        }
-    }
-    wave_sync_lds();
-    const uintptr_t pbase = reinterpret_cast<uintptr_t>(p.px);
-    const uint32_t base_off = (uint32_t)(pbase & 3u);
-    const unsigned nrec = base_off + (unsigned)((long long)(p.in_rows - 1) * p.rowstride) +
-                          (unsigned)(p.w * BPP);
-    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(pbase - base_off), (short)0, (int)nrec, (int)kBufFlags);
-    // liblqr luma (src/render.c:315, LQR_ER_LUMA) [liblqr, unverified] in the
-    // reference's order ((k_r r + k_g g) + k_b b); preview: RGB2LUMINANCE
-    auto luma3 = [&](uint32_t c0, uint32_t c1, uint32_t c2) -> double {
-        if constexpr (SEM == kSemLqr) {
-            if constexpr (BPP == 1) return lut[c0];
-            else return lut[c0] + lut[256 + c1] + lut[512 + c2];
-        } else {
-            return (double)preview_luma(c0, c1, c2, BPP);
-        }
-    };
-    const unsigned spt = (unsigned)tp.tile_w / 64u;   // strips per map tile
-    constexpr int NW = (8 * BPP + 3) / 4 + 1;         // dwords of a row's 8 pixels, any alignment
-    for (unsigned k = blockIdx.x; k < ndirty; k += gridDim.x) {   // uniform
-        const unsigned strip = p.dirty_list[k];
-        const unsigned cnt = p.tile_count[strip];
-        if (cnt <= kFixDirect<N>) continue;            // sparse: dcte_fix_strips
-        const unsigned tile = strip / spt;
-        const int bx = (int)(tile % (unsigned)tp.tiles_x), by = (int)(tile / (unsigned)tp.tiles_x);
-        const int sx0 = bx * tp.tile_w + 64 * (int)(strip % spt);
-        const int ys = p.y0 + by * p.tile_h;
-        const unsigned* list = p.fix_list + (size_t)strip * (size_t)(64 * p.tile_h);
-        for (unsigned q0 = 0; q0 < cnt; q0 += 64) {   // uniform
-            const unsigned q = q0 + (unsigned)lane;
-            if (q >= cnt) continue;
-            const unsigned loc = list[q];
-            const int lx = (int)(loc & 63), ly = (int)(loc >> 6);
-            const int x = sx0 + lx, y = ys + ly;
-            const int gx0 = x - HL;
-            const bool inside = gx0 >= 0 && gx0 + 8 <= p.w;
-            // rows in batches of RB: a batch's loads are issued, then its
-            // bytes converted (liblqr: each row's first-pass step right away
-            // -- the reference's first pass runs along x for each window row,
-            // src/fft2d/shrtdct.c:62-89, so it needs that row alone)
-            constexpr int RB = DCTE_DENSE8_RB;
-            double d[64];
-#pragma unroll
-            for (int r0 = 0; r0 < 8; r0 += RB) {
-                uint32_t fv[RB][NW];
-                uint32_t foff[RB];
-                bool fast[RB];
-#pragma unroll
-                for (int rr = 0; rr < RB; rr++) {
-                    const int gy = clampi(y - HL + r0 + rr, 0, p.h - 1);
-                    const uint32_t s0 = base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
-                                        (uint32_t)(gx0 * BPP);
-                    fast[rr] = inside && ((s0 + 8 * BPP - 1) | 3u) < nrec;
-                    foff[rr] = s0 & 3u;
-                    const uint32_t a = fast[rr] ? (s0 & ~3u) : 0x7ffffff0u;   // past num_records: zeros
-#pragma unroll
-                    for (int j = 0; j < NW; j++)
-                        fv[rr][j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * j), 0, 0);
-                }
-#pragma unroll
-                for (int rr = 0; rr < RB; rr++) {
-                    const int r = r0 + rr;
-                    double lv[8];
-                    if (fast[rr]) {
-                        uint32_t wd[NW - 1];
-#pragma unroll
-                        for (int j = 0; j < NW - 1; j++)
-                            wd[j] = __builtin_amdgcn_alignbyte(fv[rr][j + 1], fv[rr][j], foff[rr]);
-#pragma unroll
-                        for (int c = 0; c < 8; c++) {
-                            auto byte = [&](int b) { return (wd[b >> 2] >> (8 * (b & 3))) & 255u; };
-                            lv[c] = luma3(byte(c * BPP), BPP > 1 ? byte(c * BPP + 1) : 0u,
-                                          BPP > 1 ? byte(c * BPP + 2) : 0u);
-                        }
-                    } else {
-                        // clamped at the left / right frame border, or at the
-                        // frame's last bytes: per-pixel reads
-                        const int gy = clampi(y - HL + r, 0, p.h - 1);
-                        const uint8_t* row = p.px + (long long)(gy - p.in_row0) * p.rowstride;
-#pragma unroll
-                        for (int c = 0; c < 8; c++) {
-                            const uint8_t* q8 = row + (long long)clampi(gx0 + c, 0, p.w - 1) * BPP;
-                            lv[c] = luma3(q8[0], BPP > 1 ? q8[1] : 0u, BPP > 1 ? q8[2] : 0u);
-                        }
-                    }
-                    if constexpr (SEM == kSemLqr && DCTE_DENSE8_FUSE) r64::step8(lv, 1);
-                    // image row r, pixel c: liblqr data[c][r], preview data[r][c]
-#pragma unroll
-                    for (int c = 0; c < 8; c++) d[SEM == kSemLqr ? c * 8 + r : r * 8 + c] = lv[c];
-                }
-            }
-            double m;
-            bool edge;
-            if constexpr (DCTE_DENSE8_SKIP) {
-                if constexpr (!(SEM == kSemLqr && DCTE_DENSE8_FUSE)) {
-#pragma unroll
-                    for (int i = 0; i < 8; i++) {
-                        r64::step8(d + i, 8);
-                        __builtin_amdgcn_sched_barrier(0);
-                    }
-                }
-                refine8_second_skip(d, m, edge);
-            } else if constexpr (SEM == kSemLqr && DCTE_DENSE8_FUSE) {
-                refine_regs<8, DCTE_FIX_IL, false>(d, tp.ct, m, edge);
-            } else {
-                refine_regs<8>(d, tp.ct, m, edge);
-            }
-            p.out[(long long)(y - p.y0) * p.out_stride + x] =
-                edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
-        }
-    }
-}
-
 // ------------------------------------------------------------------ windows
 // dctNxN + weighted_max_dct_correlation (src/dct.c:77-110) on windows the
 // caller filled -- the per-window form of the callback (src/render.c:146-155
@@ -1766,10 +1798,7 @@ static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
         if (dev >= 0 && dev < kMaxDevices) cache[dev].store(resident, std::memory_order_relaxed);
     }
     const int blocks = nstrips < resident ? nstrips : resident;
-    hipLaunchKernelGGL((dcte_fix_strips<N, BPP, SEM>), dim3(blocks), dim3(64), 0, s, p);
     if constexpr (N == 8 && DCTE_FIX_LANES) {
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
         static std::atomic<int> dcache[kMaxDevices];
         int dres = dev >= 0 && dev < kMaxDevices ? dcache[dev].load(std::memory_order_relaxed) : 0;
         if (!dres) {
@@ -1784,8 +1813,19 @@ static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
             if (dev >= 0 && dev < kMaxDevices) dcache[dev].store(dres, std::memory_order_relaxed);
         }
         const int dblocks = nstrips < dres ? nstrips : dres;
+        if constexpr (DCTE_FIX_MERGE) {
+            TileFixParams q = p;
+            q.sparse_blocks = blocks;
+            hipLaunchKernelGGL((dcte_fix_strips<N, BPP, SEM>), dim3(blocks + dblocks), dim3(64), 0, s, q);
+            return hipGetLastError();
+        }
+        hipLaunchKernelGGL((dcte_fix_strips<N, BPP, SEM>), dim3(blocks), dim3(64), 0, s, p);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
         hipLaunchKernelGGL((dcte_fix_dense8<BPP, SEM>), dim3(dblocks), dim3(64), 0, s, p);
+        return hipGetLastError();
     }
+    hipLaunchKernelGGL((dcte_fix_strips<N, BPP, SEM>), dim3(blocks), dim3(64), 0, s, p);
     return hipGetLastError();
 }
 

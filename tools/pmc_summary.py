@@ -37,7 +37,7 @@ def main():
     src, rnd = sys.argv[1], sys.argv[2]
     size = int(sys.argv[sys.argv.index("--size") + 1]) if "--size" in sys.argv else 16384
     n = int(sys.argv[sys.argv.index("--n") + 1]) if "--n" in sys.argv else 8
-    kname = f"dcte_map<{n}, 3, 0>"
+    kname = f"dcte_map<{n}, 3, 0"   # template args may follow (", false>")
     dst = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(dst, exist_ok=True)
     def opt_list(flag):
