@@ -76,6 +76,12 @@ namespace dcte {
 #ifndef DCTE_XBAL
 #define DCTE_XBAL 1        // halo-column luma conversions spread one per lane of the last wave
 #endif
+#ifndef DCTE_CONV_BAL
+#define DCTE_CONV_BAL 0    // N = 16: luma conversions spread over all threads of the workgroup
+#endif
+#ifndef DCTE_EMIT_NB
+#define DCTE_EMIT_NB 0     // store without a branch on the column (out-of-frame lanes dropped by the bounds check)
+#endif
 #ifndef DCTE_DIRECT
 #define DCTE_DIRECT 1      // N = 8: each lane loads its own pixel's bytes (dwordx2), no raw LDS stage (-1.8 %)
 #endif
@@ -309,9 +315,9 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
     const float we = p.we, wt = p.wt;
     // output rows [ys, ye) of this workgroup through one buffer resource
     const int ostride4 = (int)(p.out_stride * 4);
+    const uint32_t orec = (unsigned)(max(ye - ys - 1, 0)) * (unsigned)ostride4 + (unsigned)w * 4u;
     __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
-        p.out + (long long)(ys - p.y0) * p.out_stride, (short)0,
-        (int)((unsigned)(max(ye - ys - 1, 0)) * (unsigned)ostride4 + (unsigned)w * 4u), (int)kBufFlags);
+        p.out + (long long)(ys - p.y0) * p.out_stride, (short)0, (int)orec, (int)kBufFlags);
     // refinement lists of this tile's strips (dcte_fix_strips); nflag is set
     // before the first barrier and read after the last one
     const int sc = S == 1 ? c >> 6 : 0;              // this thread's strip in the tile
@@ -328,18 +334,28 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
 
     // decision + store (+ refinement flag) of output pixel (x, y)
     auto emit = [&](int y, int xx, float mt, float me) {
+#if DCTE_EMIT_NB
+        // no branch on the column: a lane past the frame's last column stores
+        // at the resource's size, which the bounds check drops (the wave's
+        // row offset rides in soffset, so the sum stays below 2^32)
+        const bool inside = xx < w;
+        const uint32_t voff = inside ? (uint32_t)xx * 4u : orec;
+#else
         if (xx >= w) return;
+        const bool inside = true;
+        const uint32_t voff = (uint32_t)xx * 4u;
+#endif
         const bool edge = me > mt;
         // the product, then the select (the weights stay in SGPRs)
         const float e_out = me * we, t_out = mt * wt;
         // row offset is wave-uniform (soffset), column offset per lane
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(edge ? e_out : t_out), orsrc,
-                                              xx * 4, (y - ys) * ostride4, 0);
+                                              (int)voff, (y - ys) * ostride4, 0);
         // refine in fp64 when the class is uncertain: the smaller maximum
         // within the fp32 error band of the larger, lo > (1 - tau) hi, i.e.
         // me > keep mt AND mt > keep me (never for all-zero windows); every
         // pixel when tie_tau >= 1 (testing)
-        if ((check_ties && me > keep * mt && mt > keep * me) || force_all) {
+        if (inside && ((check_ties && me > keep * mt && mt > keep * me) || force_all)) {
             const unsigned k = atomicAdd(&nflag[sc], 1u);      // < 64 * tile_h
             strip_list[k] = (unsigned)((y - ys) * 64 + (xx - sx0));
         }
@@ -394,6 +410,11 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
             for (int u = 0; u < G; u++) luma_at(gg, b, u, tx);
             const int l = tx - (kThreads - 64);
             if (l >= 0 && l < X * G) luma_at(gg, b, l / X, kThreads + l % X);
+        } else if constexpr (DCTE_CONV_BAL && LW < kThreads) {
+            // fewer columns than threads (N = 16: 79 of 256): the LW x G
+            // conversions spread over every thread, not G rows on LW threads
+            // (which held two waves busy while two idled before the barrier)
+            for (int e = tx; e < LW * G; e += kThreads) luma_at(gg, b, e / LW, e % LW);
         } else {
             for (int cc = tx; cc < LW; cc += kThreads) {
 #pragma unroll
