@@ -80,7 +80,7 @@ namespace dcte {
 #define DCTE_CONV_BAL 0    // N = 16: luma conversions spread over all threads of the workgroup
 #endif
 #ifndef DCTE_EMIT_NB
-#define DCTE_EMIT_NB 0     // store without a branch on the column (out-of-frame lanes dropped by the bounds check)
+#define DCTE_EMIT_NB 1     // store without a branch on the column (out-of-frame lanes dropped by the bounds check)
 #endif
 #ifndef DCTE_DIRECT
 #define DCTE_DIRECT 1      // N = 8: each lane loads its own pixel's bytes (dwordx2), no raw LDS stage (-1.8 %)
