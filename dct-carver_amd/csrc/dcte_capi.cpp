@@ -26,6 +26,7 @@ namespace {
 
 constexpr double kDefaultTieTau = 4e-6;
 constexpr int kMaxGridY = 65535;   // launch grid limit in y (map tiles of a band)
+constexpr int kCountWords = 8;     // FixScratch::d_count
 #ifndef DCTE_WIDE_BANDS
 #define DCTE_WIDE_BANDS 1          // DCTE_OPT_WIDE_BANDS available (off by default)
 #endif
@@ -33,13 +34,16 @@ constexpr int kMaxGridY = 65535;   // launch grid limit in y (map tiles of a ban
 struct FixScratch {
     // [0] list length (points / seam), [1] refined, [2 + phase] dirty strips of
     // the map launches (two, alternating: each map launch zeroes the other one
-    // for the next launch, so no memset is needed between launches)
+    // for the next launch, so no memset is needed between launches), [4 + 2
+    // phase] the same for the 64-bit dense-strip counter (N = 8)
     unsigned* d_count = nullptr;
     unsigned phase = 0;
     unsigned* d_list = nullptr;    // flagged pixels (map: per-tile regions)
     size_t cap = 0;
-    unsigned* d_tiles = nullptr;   // map: per-tile counts | dirty-tile list
+    unsigned* d_tiles = nullptr;   // map: per-strip counts | dirty-strip list | dense-strip pairs
     size_t tcap = 0;               // tiles
+    void* d_batch = nullptr;       // map: the dense refinement batches' strips (uint4 each)
+    size_t bcap = 0;               // bytes
 };
 
 struct DpScratch {                 // seam DP (dcte_dp.hip), per stream
@@ -176,8 +180,11 @@ int ensure_fix(dcte_ctx* ctx, Device& d, hipStream_t s, size_t npix, FixScratch*
 {
     FixScratch& f = d.fix[s];
     if (!f.d_count) {
-        DCTE_HIP(ctx, hipMalloc(&f.d_count, 4 * sizeof(unsigned)));
-        DCTE_HIP(ctx, hipMemset(f.d_count, 0, 4 * sizeof(unsigned)));
+        DCTE_HIP(ctx, hipMalloc(&f.d_count, kCountWords * sizeof(unsigned)));
+        // on the scratch's own stream: a plain hipMemset is not ordered with
+        // the (non-blocking) streams the kernels run on, and a map launch that
+        // started before it landed would count from whatever the allocation held
+        DCTE_HIP(ctx, hipMemsetAsync(f.d_count, 0, kCountWords * sizeof(unsigned), s));
     }
     if (f.cap < npix) {
         if (f.d_list) DCTE_HIP(ctx, hipFree(f.d_list));
@@ -196,7 +203,8 @@ int ensure_tiles(dcte_ctx* ctx, FixScratch* f, size_t ntiles)
     if (f->d_tiles) DCTE_HIP(ctx, hipFree(f->d_tiles));
     f->d_tiles = nullptr;
     f->tcap = 0;
-    DCTE_HIP(ctx, hipMalloc(&f->d_tiles, 2 * ntiles * sizeof(unsigned)));
+    // per-strip counts | dirty-strip list | dense-strip pairs (N = 8)
+    DCTE_HIP(ctx, hipMalloc(&f->d_tiles, 4 * ntiles * sizeof(unsigned)));
     f->tcap = ntiles;
     return DCTE_OK;
 }
@@ -252,6 +260,8 @@ dcte::FixParams fix_params(const uint8_t* px, long long rowstride, int w, int h,
     q.max_items = (unsigned)f->cap;
     return q;
 }
+
+int ensure_buf(dcte_ctx* ctx, void** p, size_t* cap, size_t bytes);
 
 int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, int w, int h,
                int bpp, int in_row0, int in_rows, int y0, int y1, int n, float edges,
@@ -313,6 +323,12 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     if (rc) return rc;
     rc = ensure_tiles(ctx, f, ntiles);
     if (rc) return rc;
+    // the dense refinement's batch map (N = 8, and N = 16 liblqr): one uint4
+    // per batch of 64 (16) entries the lists can hold
+    if (n == 8 || (n == 16 && sem == DCTE_LQR)) {
+        rc = ensure_buf(ctx, &f->d_batch, &f->bcap, (list_len / (n == 8 ? 64 : 16) + 1) * 16);
+        if (rc) return rc;
+    }
 
     const double scale = weight_scale(n, sem);
     dcte::MapParams p{};
@@ -339,6 +355,10 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     p.dirty_list = f->d_tiles + ntiles;
     p.dirty_count = f->d_count + 2 + f->phase;
     p.dirty_next = f->d_count + 2 + (f->phase ^ 1u);
+    p.dense_ctr = reinterpret_cast<unsigned long long*>(f->d_count + 4) + f->phase;
+    p.dense_next = reinterpret_cast<unsigned long long*>(f->d_count + 4) + (f->phase ^ 1u);
+    p.dense_list = reinterpret_cast<uint2*>(f->d_tiles + 2 * ntiles);
+    p.dense_batch = static_cast<uint4*>(f->d_batch);
     p.stamps = ctx->stamps;
 
     dcte::TileFixParams q{};
@@ -352,7 +372,7 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     // stream: a map launch that never ran did not zero its successor's counter,
     // and a later call must not walk an older launch's dirty list.
     auto fail = [&](hipError_t e, const char* where) {
-        (void)hipMemsetAsync(f->d_count + 2, 0, 2 * sizeof(unsigned), s);
+        (void)hipMemsetAsync(f->d_count + 2, 0, (kCountWords - 2) * sizeof(unsigned), s);
         return hip_fail(ctx, e, where);
     };
     hipError_t e = hipSuccess;
@@ -612,6 +632,7 @@ void dcte_destroy(dcte_ctx* ctx)
             if (kv.second.d_count) (void)hipFree(kv.second.d_count);
             if (kv.second.d_list) (void)hipFree(kv.second.d_list);
             if (kv.second.d_tiles) (void)hipFree(kv.second.d_tiles);
+            if (kv.second.d_batch) (void)hipFree(kv.second.d_batch);
         }
         for (auto& kv : d.dp) {
             (void)hipStreamSynchronize(kv.first);

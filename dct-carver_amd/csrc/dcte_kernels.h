@@ -37,6 +37,21 @@ struct MapParams {
     unsigned* dirty_list;
     unsigned* dirty_count;   // zero when the launch starts
     unsigned* dirty_next;    // zeroed by this launch: the next launch's dirty_count
+    // N = 8 (and N = 16 liblqr): the DENSE strips (more than kFixDirect flags)
+    // once more, as one flat work list for the dense refinement walks
+    // (fix_dense8_flat, fix_dense16_flat): *dense_ctr = {strips << 32 | entries}
+    // (zero when the launch starts; dense_next zeroed by it), and per dense
+    // strip dense_list[slot] = {strip, offset of its first entry in the
+    // concatenation} -- the offsets ascend with the slot (one 64-bit atomic
+    // hands out both)
+    unsigned long long* dense_ctr;
+    unsigned long long* dense_next;
+    uint2* dense_list;
+    // and per refinement batch b (kDenseBatch entries of the flat list,
+    // 64 at N = 8, 16 at N = 16) the dense strip holding its first entry:
+    // {its first column, its tile's first output row, strip, offset of its
+    // first entry in the flat list}
+    uint4* dense_batch;
     // timing-probe builds only (DCTE_TSTAMP): 3 words per workgroup {start,
     // end, HW_ID}, a buffer nothing else reads (null: no stamps)
     unsigned long long* stamps;

@@ -87,6 +87,32 @@ namespace dcte {
 #endif
 constexpr unsigned kBufFlags = 0x00020000u;  // gfx9 raw buffer dword3
 
+// refinement (below): strips with at most kFixDirect<N> flagged pixels are
+// "sparse" (dcte_fix_strips gathers their windows directly), the rest dense
+#ifndef DCTE_FIX_LANES
+#define DCTE_FIX_LANES 1 // dense strips at N = 8: one lane per pixel, window in registers
+#endif
+#ifndef DCTE_FIX_FLAT
+#define DCTE_FIX_FLAT 1  // ... taken from one flat list of all dense entries, 64 at a time, pipelined
+#endif
+template <int N>
+constexpr unsigned kFixDirect = N == 16 ? 32u : 128u;
+#ifndef DCTE_FIX_QUAD16
+#define DCTE_FIX_QUAD16 1 // dense strips at N = 16 (liblqr): four lanes per pixel, window in registers
+#endif
+// dense strips walked by a lane-per-pixel / lane-quad-per-pixel kernel of
+// their own (fix_dense8*, fix_dense16_flat) rather than the band path of
+// dcte_fix_strips
+template <int N, int SEM>
+constexpr bool kDenseOwn = (N == 8 && DCTE_FIX_LANES) || (N == 16 && SEM == kSemLqr && DCTE_FIX_QUAD16);
+// ... from the flat list the map kernel numbers (MapParams::dense_list)
+template <int N, int SEM>
+constexpr bool kDenseFlat = (N == 8 && DCTE_FIX_LANES && DCTE_FIX_FLAT) || (N == 16 && kDenseOwn<N, SEM>);
+// entries per refinement batch of the flat list: a lane per pixel at N = 8,
+// a quad of lanes at N = 16
+template <int N>
+constexpr unsigned kDenseBatch = N == 8 ? 64u : 16u;
+
 // SEM = kSemLqr    : liblqr callback window, offsets -(N/2-1)..N/2
 //                    (src/render.c:146-152), liblqr luma (dcte_luma.h)
 // SEM = kSemPreview: GTK preview window, offsets -(c-1)..N-c with
@@ -165,6 +191,8 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
     // refinement lists per 64-column strip (one wave's columns; N = 16: the tile)
     constexpr int SPT = S == 1 ? TW / 64 : 1;        // strips per tile
     __shared__ unsigned nflag[SPT];                  // pixels each strip flagged
+    __shared__ uint4 dense_sh[kDenseFlat<N, SEM> ? SPT : 1];   // dense strips' batch-map entries
+    __shared__ unsigned dense_cnt[kDenseFlat<N, SEM> ? SPT : 1];
 
     const int tx = threadIdx.x;
     const int lane_p = (S == 4) ? (tx >> 6) : 0;     // N = 16: wave index = k1 class
@@ -325,9 +353,13 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
     unsigned* strip_list = p.fix_list + (size_t)strip * (size_t)(64 * p.tile_h);
     const int sx0 = x0 + 64 * sc;                    // first column of the strip
     if (tx < SPT) nflag[tx] = 0;
-    // the next launch's dirty-strip counter (stream order: nothing reads it
-    // before this launch ends)
-    if (tx == 0 && blockIdx.x == 0 && blockIdx.y == 0) *p.dirty_next = 0u;
+    // the next launch's dirty-strip and dense counters (stream order: nothing
+    // reads them before this launch ends) -- in every launch, whatever its N
+    // or semantics: the phases alternate over all launches of the stream
+    if (tx == 0 && blockIdx.x == 0 && blockIdx.y == 0) {
+        *p.dirty_next = 0u;
+        *p.dense_next = 0ull;
+    }
     const bool check_ties = we != wt;                // uniform
     const bool force_all = p.tie_tau >= 1.0f;        // uniform
     const float keep = 1.0f - p.tie_tau;             // |me - mt| <= tau * hi  <=>  lo >= (1 - tau) hi
@@ -580,10 +612,45 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
         }
     }
     __syncthreads();
-    if (tx < SPT && nflag[tx]) {
-        const unsigned st = strip - sc + tx;
-        p.tile_count[st] = nflag[tx];
-        p.dirty_list[atomicAdd(p.dirty_count, 1u)] = st;
+    if (tx < SPT) {
+        uint4 di = make_uint4(0u, 0u, 0u, 0u);
+        unsigned dcnt = 0;                             // 0: not a dense strip
+        const unsigned cnt = nflag[tx];
+        if (cnt) {
+            const unsigned st = strip - sc + tx;
+            p.tile_count[st] = cnt;
+            p.dirty_list[atomicAdd(p.dirty_count, 1u)] = st;
+            if (kDenseFlat<N, SEM> && cnt > kFixDirect<N>) {
+                const unsigned long long r = atomicAdd(p.dense_ctr, (1ull << 32) | cnt);
+                const unsigned slot = (unsigned)(r >> 32), off = (unsigned)r;
+                // a launch holds gridDim.x * gridDim.y * SPT strips (the guard only
+                // matters if the counter did not start at zero)
+                if (slot < gridDim.x * gridDim.y * SPT) {
+                    p.dense_list[slot] = make_uint2(st, off);
+                    di = make_uint4((unsigned)(x0 + 64 * tx), (unsigned)ys, st, off);
+                    dcnt = cnt;
+                }
+            }
+        }
+        if constexpr (kDenseFlat<N, SEM>) {
+            dense_sh[tx] = di;
+            dense_cnt[tx] = dcnt;
+        }
+    }
+    if constexpr (kDenseFlat<N, SEM>) {
+        // the batch map: every refinement batch (kDenseBatch<N> entries of the
+        // flat list) whose first entry lies in one of this workgroup's dense
+        // strips points at that strip, so a wave finds any batch in one load
+        __syncthreads();
+        constexpr unsigned EPB = kDenseBatch<N>;
+#pragma unroll
+        for (int k = 0; k < SPT; k++) {
+            const uint4 di = dense_sh[k];
+            const unsigned cnt = dense_cnt[k];
+            if (cnt == 0u) continue;                   // uniform
+            const unsigned first = (di.w + EPB - 1u) / EPB, last = (di.w + cnt - 1u) / EPB;
+            for (unsigned b = first + (unsigned)tx; b <= last; b += (unsigned)kThreads) p.dense_batch[b] = di;
+        }
     }
 #if DCTE_TSTAMP
     // timing probe builds only (tools/tstamp.py): the workgroup's start /
@@ -874,8 +941,6 @@ __global__ __launch_bounds__(kFixThreads) void dcte_fix(const FixParams p)
 // at 128 (dots on flat ground, 0.37 % flagged at 16384^2: 0.31 ms vs 0.58 at
 // 32; line art unchanged, worse from 256), N = 16 at 32
 // (profiles/r02/fix_direct.jsonl).
-template <int N>
-constexpr unsigned kFixDirect = N == 16 ? 32u : 128u;
 #ifndef DCTE_FIX_ALIGNED
 #define DCTE_FIX_ALIGNED 1  // dense strips read the staged raw bytes as aligned dwords
 #endif
@@ -938,9 +1003,6 @@ __device__ __forceinline__ void refine_group(const double* lum, int LW, int at, 
                       w, l, best, edge);
 }
 
-#ifndef DCTE_FIX_LANES
-#define DCTE_FIX_LANES 1 // dense strips at N = 8: one lane per pixel, window in registers
-#endif
 #ifndef DCTE_FIX_MERGE
 #define DCTE_FIX_MERGE 1 // ... run by extra blocks of the dcte_fix_strips launch (one launch less)
 #endif
@@ -968,6 +1030,12 @@ constexpr int kFixMinWaves = (BPP == 1 && N <= 8) ? ((N == 8 && DCTE_FIX_LANES) 
 #ifndef DCTE_DENSE8_MINW
 #define DCTE_DENSE8_MINW 2
 #endif
+#ifndef DCTE_DENSE8_PF
+#define DCTE_DENSE8_PF 1        // flat walk: a batch's window rows load during the previous batch
+#endif
+#ifndef DCTE_DENSE8_PF_GREY
+#define DCTE_DENSE8_PF_GREY 0   // ... not for grey layers (162 VGPRs: 3 waves per SIMD)
+#endif
 #ifndef DCTE_DENSE8_RB
 #define DCTE_DENSE8_RB 8      // window rows per load batch
 #endif
@@ -976,6 +1044,11 @@ constexpr int kFixMinWaves = (BPP == 1 && N <= 8) ? ((N == 8 && DCTE_FIX_LANES) 
 #endif
 #ifndef DCTE_DENSE8_SKIP
 #define DCTE_DENSE8_SKIP 0    // skip second-pass rows whose norm is below the running maximum
+#endif
+// timing-probe builds only (wrong results): 1 = no table reads (luma = first
+// byte), 2 = no transform, 3 = no row loads
+#ifndef DCTE_DENSE8_PROBE
+#define DCTE_DENSE8_PROBE 0
 #endif
 // the 256 liblqr channel quotients v / 255 (pre-weighted per channel for
 // liblqr RGB: kTab), as the reference divides (bit-identical)
@@ -1016,6 +1089,7 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
     // liblqr luma (src/render.c:315, LQR_ER_LUMA) [liblqr, unverified] in the
     // reference's order ((k_r r + k_g g) + k_b b); preview: RGB2LUMINANCE
     auto luma3 = [&](uint32_t c0, uint32_t c1, uint32_t c2) -> double {
+        if constexpr (DCTE_DENSE8_PROBE == 1) return (double)(c0 + c1 + c2);
         if constexpr (SEM == kSemLqr) {
             if constexpr (BPP == 1) return lut[c0];
             else return lut[c0] + lut[256 + c1] + lut[512 + c2];
@@ -1063,7 +1137,8 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
                     const uint32_t a = fast[rr] ? (s0 & ~3u) : 0x7ffffff0u;   // past num_records: zeros
 #pragma unroll
                     for (int j = 0; j < NW; j++)
-                        fv[rr][j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * j), 0, 0);
+                        fv[rr][j] = DCTE_DENSE8_PROBE == 3 ? ((a & 4u) ? 0xffffffffu : 0u)
+                                                           : __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * j), 0, 0);
                 }
 #pragma unroll
                 for (int rr = 0; rr < RB; rr++) {
@@ -1099,7 +1174,12 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
             }
             double m;
             bool edge;
-            if constexpr (DCTE_DENSE8_SKIP) {
+            if constexpr (DCTE_DENSE8_PROBE == 2) {
+                m = 0.0;
+#pragma unroll
+                for (int i = 0; i < 64; i++) m += d[i];
+                edge = false;
+            } else if constexpr (DCTE_DENSE8_SKIP) {
                 if constexpr (!(SEM == kSemLqr && DCTE_DENSE8_FUSE)) {
 #pragma unroll
                     for (int i = 0; i < 8; i++) {
@@ -1119,15 +1199,512 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
     }
 }
 
+// The same refinement over ONE flat list: the map kernel numbered the dense
+// strips' entries consecutively (MapParams::dense_list), so wave `blk` of
+// `nblk` takes a contiguous run of 64-entry batches -- every wave gets the
+// same number of full batches whatever the strips' counts, and a batch spans
+// at most two strips (a dense strip holds more than 128 entries).  Three
+// batches are in flight per wave: batch b is transformed while batch b + 1's
+// window rows and batch b + 2's list words load.
+template <int BPP>
+struct D8Rows {
+    static constexpr int NW = (8 * BPP + 3) / 4 + 1;  // dwords of a row's 8 pixels, any alignment
+    uint32_t fv[8][NW];
+    uint32_t foff;      // 2 bits per row: byte offset of the row's first pixel in fv[r][0]
+    uint32_t fast;      // bit per row: fv holds the row (else per-pixel reads)
+    int x, y;
+    bool valid;
+};
+
+// Cursor over the flat dense list for one wave: batches of EPB entries,
+// the wave taking batches blk, blk + nblk, ... -- the waves resident at one
+// time work on neighbouring batches (neighbouring strips, so their window rows
+// share the L2), every wave gets the same number of full batches whatever the
+// strips' counts.  A batch's first strip comes from the map kernel's batch
+// map (MapParams::dense_batch); a batch spans at most two strips (a dense
+// strip holds more than kFixDirect >= EPB entries), the second one is the
+// next slot of dense_list.
+#ifndef DCTE_DENSE_CHUNK
+#define DCTE_DENSE_CHUNK 8      // consecutive refinement batches per wave before it strides on
+#endif
+template <int EPB>
+struct DenseWalk {
+    const TileFixParams* tp;
+    unsigned total, nb, b0, step, per_strip, chunk;
+
+    // false: no batch for this wave
+    __device__ __forceinline__ bool init(const TileFixParams& t, unsigned blk, unsigned nblk)
+    {
+        tp = &t;
+        const MapParams& p = t.m;
+        const unsigned long long dc = *p.dense_ctr;
+        const unsigned nd = (unsigned)(dc >> 32);
+        total = (unsigned)dc;
+        per_strip = 64u * (unsigned)p.tile_h;
+        // the map launch numbered at most this many strips (a counter that did
+        // not start at zero must not send the walk past the lists)
+        const unsigned nstrips = (unsigned)t.tiles_x * ((unsigned)t.tile_w / 64u) *
+                                 (unsigned)((p.y1 - p.y0 + p.tile_h - 1) / p.tile_h);
+        if (nd > nstrips || total > nstrips * per_strip) return false;   // uniform
+        nb = (total + EPB - 1) / EPB;
+        // chunks of up to DCTE_DENSE_CHUNK consecutive batches while every
+        // wave still gets several (fewer batches: one at a time, all waves busy)
+        chunk = min(max(nb / nblk, 1u), (unsigned)DCTE_DENSE_CHUNK);
+        b0 = blk * chunk;
+        step = nblk;
+        return b0 < nb;
+    }
+
+    // the wave's batch after b (>= nb: none): chunk blk, blk + nblk, ... of
+    // `chunk` consecutive batches -- a chunk's batches share window rows in
+    // the wave's L1, the resident waves' chunks neighbour each other in the L2
+    __device__ __forceinline__ unsigned next(unsigned b) const
+    {
+        return ((b + 1) % chunk != 0 && b + 1 < nb) ? b + 1 : (b / chunk + step) * chunk;
+    }
+
+    // batch b's entry of the batch map (b < nb): {first column, first output
+    // row, strip, offset of its first entry in the flat list} of the strip
+    // holding entry EPB b; loaded a batch ahead of its list()
+    __device__ __forceinline__ uint4 info(unsigned b) const { return tp->m.dense_batch[b]; }
+
+    // batch b's list word of entry EPB b + q (q < EPB); A = info(b), B =
+    // info(b + 1) (b + 1 < nb; else A): a batch whose last entries lie in the
+    // next strip finds that strip as the first one of batch b + 1 (a dense
+    // strip holds more than EPB entries)
+    __device__ __forceinline__ void list(unsigned b, const uint4& A, const uint4& B, unsigned q, unsigned& loc,
+                                         int& sx0, int& ys, bool& valid) const
+    {
+        const unsigned e = b * EPB + q;
+        valid = e < total;
+        const bool up = B.z != A.z && e >= B.w;
+        sx0 = (int)(up ? B.x : A.x);
+        ys = (int)(up ? B.y : A.y);
+        const unsigned idx = up ? B.z * per_strip + (e - B.w) : A.z * per_strip + (e - A.w);
+        loc = tp->m.fix_list[valid ? idx : A.z * per_strip];
+    }
+};
+
+template <int BPP, int SEM>
+__device__ __forceinline__ void fix_dense8_flat(const TileFixParams& tp, const double* lut,
+                                                unsigned blk, unsigned nblk)
+{
+    constexpr int N = 8;
+    constexpr int HL = Geo<N, SEM>::HL;
+    constexpr int NW = D8Rows<BPP>::NW;
+    const MapParams& p = tp.m;
+    DenseWalk<64> dw;
+    if (!dw.init(tp, blk, nblk)) return;               // uniform
+    const unsigned b0 = dw.b0, nb = dw.nb;
+    const int lane = threadIdx.x;
+    const uintptr_t pbase = reinterpret_cast<uintptr_t>(p.px);
+    const uint32_t base_off = (uint32_t)(pbase & 3u);
+    const unsigned nrec = base_off + (unsigned)((long long)(p.in_rows - 1) * p.rowstride) +
+                          (unsigned)(p.w * BPP);
+    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(pbase - base_off), (short)0, (int)nrec, (int)kBufFlags);
+    // liblqr luma (src/render.c:315, LQR_ER_LUMA) [liblqr, unverified] in the
+    // reference's order ((k_r r + k_g g) + k_b b); preview: RGB2LUMINANCE
+    auto luma3 = [&](uint32_t c0, uint32_t c1, uint32_t c2) -> double {
+        if constexpr (DCTE_DENSE8_PROBE == 1) return (double)(c0 + c1 + c2);
+        if constexpr (SEM == kSemLqr) {
+            if constexpr (BPP == 1) return lut[c0];
+            else return lut[c0] + lut[256 + c1] + lut[512 + c2];
+        } else {
+            return (double)preview_luma(c0, c1, c2, BPP);
+        }
+    };
+    // batch-map entries of the next list_stage's batch b and of b + 1
+    uint4 infA = dw.info(b0), infB = b0 + 1 < nb ? dw.info(b0 + 1) : infA;
+    auto list_stage = [&](unsigned b, unsigned& loc, int& sx0, int& ys, bool& valid) {
+        const uint4 A = infA, B = infB;
+        const unsigned bn = dw.next(b);
+        if (bn < nb) {                                 // uniform
+            infA = dw.info(bn);
+            infB = bn + 1 < nb ? dw.info(bn + 1) : infA;
+        }
+        dw.list(b, A, B, (unsigned)lane, loc, sx0, ys, valid);
+    };
+    // batch's window rows: the eight image rows as whole dwords through the
+    // frame's buffer resource (per-pixel reads where the window is clamped at
+    // the left / right border or reaches the frame's last bytes)
+    auto row_stage = [&](unsigned loc, int sx0, int ys, bool valid, D8Rows<BPP>& R) {
+        R.x = sx0 + (int)(loc & 63u);
+        R.y = ys + (int)(loc >> 6);
+        R.valid = valid;
+        const int gx0 = R.x - HL;
+        const bool inside = valid && gx0 >= 0 && gx0 + 8 <= p.w;
+        R.fast = 0;
+        R.foff = 0;
+#pragma unroll
+        for (int rr = 0; rr < 8; rr++) {
+            const int gy = clampi(R.y - HL + rr, 0, p.h - 1);
+            const uint32_t s0 = base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
+                                (uint32_t)(gx0 * BPP);
+            const bool fast = inside && ((s0 + 8 * BPP - 1) | 3u) < nrec;
+            R.fast |= (uint32_t)fast << rr;
+            R.foff |= (s0 & 3u) << (2 * rr);
+            const uint32_t a = fast ? (s0 & ~3u) : 0x7ffffff0u;   // past num_records: zeros
+#pragma unroll
+            for (int j = 0; j < NW; j++)
+                R.fv[rr][j] = DCTE_DENSE8_PROBE == 3 ? ((a & 4u) ? 0xffffffffu : 0u)
+                                                     : __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * j), 0, 0);
+        }
+    };
+    auto convert = [&](const D8Rows<BPP>& R, double (&d)[64]) {
+        const int gx0 = R.x - HL;
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            double lv[8];
+            // lanes without an entry decode their (zero) fetch like a fast row
+            if (((R.fast >> r) & 1u) || !R.valid) {
+                const uint32_t fo = (R.foff >> (2 * r)) & 3u;
+                uint32_t wd[NW - 1];
+#pragma unroll
+                for (int j = 0; j < NW - 1; j++) wd[j] = __builtin_amdgcn_alignbyte(R.fv[r][j + 1], R.fv[r][j], fo);
+#pragma unroll
+                for (int c = 0; c < 8; c++) {
+                    auto byte = [&](int b) { return (wd[b >> 2] >> (8 * (b & 3))) & 255u; };
+                    lv[c] = luma3(byte(c * BPP), BPP > 1 ? byte(c * BPP + 1) : 0u, BPP > 1 ? byte(c * BPP + 2) : 0u);
+                }
+            } else {
+                // (opaque copies: the compiler would otherwise hoist these
+                // addresses out of the rare branch into every batch)
+                int xs = gx0, yr = R.y - HL + r;
+                asm volatile("" : "+v"(xs), "+v"(yr));
+                const int gy = clampi(yr, 0, p.h - 1);
+                const uint8_t* row = p.px + (long long)(gy - p.in_row0) * p.rowstride;
+#pragma unroll
+                for (int c = 0; c < 8; c++) {
+                    const uint8_t* q8 = row + (long long)clampi(xs + c, 0, p.w - 1) * BPP;
+                    lv[c] = luma3(q8[0], BPP > 1 ? q8[1] : 0u, BPP > 1 ? q8[2] : 0u);
+                }
+            }
+            // image row r, pixel c: liblqr data[c][r], preview data[r][c]
+#pragma unroll
+            for (int c = 0; c < 8; c++) d[SEM == kSemLqr ? c * 8 + r : r * 8 + c] = lv[c];
+        }
+    };
+
+    // rows one batch ahead (kPF), or loaded at their batch -- grey windows
+    // without the 24 prefetch registers fit three waves per SIMD, which the
+    // compute-bound dense grey frames prefer
+    constexpr bool kPF = BPP == 1 ? DCTE_DENSE8_PF_GREY : DCTE_DENSE8_PF;
+    unsigned locN = 0;
+    int sxN = 0, ysN = 0;
+    bool vN = false;
+    D8Rows<BPP> R;
+    {
+        unsigned loc0;
+        int sx, ys;
+        bool v;
+        list_stage(b0, loc0, sx, ys, v);
+        if (dw.next(b0) < nb) list_stage(dw.next(b0), locN, sxN, ysN, vN);
+        if constexpr (kPF) row_stage(loc0, sx, ys, v, R);
+        else { R.x = sx; R.y = ys; R.valid = v; R.fast = loc0; }   // parked: batch b0's list word
+    }
+    for (unsigned b = b0; b < nb; b = dw.next(b)) {    // uniform
+        double d[64];
+        if constexpr (!kPF) {
+            const unsigned loc = R.fast;
+            row_stage(loc, R.x, R.y, R.valid, R);
+        }
+        convert(R, d);
+        const int x = R.x, y = R.y;
+        const bool v = R.valid;
+        // the next batch's loads reuse R's registers: not above the convert
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned bn = dw.next(b);
+        if (bn < nb) {                                 // uniform
+            if constexpr (kPF) {
+                row_stage(locN, sxN, ysN, vN, R);
+            } else {
+                R.x = sxN;
+                R.y = ysN;
+                R.valid = vN;
+                R.fast = locN;
+            }
+            if (dw.next(bn) < nb) list_stage(dw.next(bn), locN, sxN, ysN, vN);
+        }
+        double m;
+        bool edge;
+        if constexpr (DCTE_DENSE8_PROBE == 2) {
+            m = 0.0;
+#pragma unroll
+            for (int i = 0; i < 64; i++) m += d[i];
+            edge = false;
+        } else {
+            refine_regs<8>(d, tp.ct, m, edge);
+        }
+        if (v)
+            p.out[(long long)(y - p.y0) * p.out_stride + x] =
+                edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
+    }
+}
+
+template <int BPP, int SEM>
+__device__ __forceinline__ void fix_dense8(const TileFixParams& tp, const double* lut, unsigned blk, unsigned nblk)
+{
+#if DCTE_FIX_FLAT
+    fix_dense8_flat<BPP, SEM>(tp, lut, blk, nblk);
+#else
+    fix_dense8_run<BPP, SEM>(tp, lut, blk, nblk);
+#endif
+}
+
+// ---- N = 16 dense strips (liblqr): four lanes per pixel ----------------
+// 256 doubles do not fit one lane, so a window is split over the four rows
+// (16 lanes each) of the wave: lane 16 q + w holds window lines 4q .. 4q + 3
+// of pixel slot w (liblqr data[dx][dy]: line j = image row y - 7 + j, 16
+// pixels along x), 64 doubles in registers.  The reference's first pass
+// (ddct16x16s along the first index for each line, src/fft2d/shrtdct.c:
+// 239-313) needs only the lane's own lines; the second pass needs whole
+// coefficient rows k1, so the 16 x 16 block of first-pass outputs is
+// transposed across the four rows with the gfx950 row swaps
+// (v_permlane32_swap: rows 2-3 of one register <-> rows 0-1 of another;
+// v_permlane16_swap: odd rows <-> even rows), 4 x 4 blocks of doubles at a
+// time, no LDS: afterwards lane 16 q + w holds rows k1 = 4q .. 4q + 3.  The
+// last-maximum scan (src/dct.c:100-108) reduces the four rows' maxima.
+
+// the register swaps of one double (two dwords each)
+__device__ __forceinline__ void swap_rows32(double& x, double& y)
+{
+    const unsigned long long a = (unsigned long long)__double_as_longlong(x);
+    const unsigned long long b = (unsigned long long)__double_as_longlong(y);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)a, (unsigned)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(a >> 32), (unsigned)(b >> 32), false, false);
+    x = __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));
+    y = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));
+}
+__device__ __forceinline__ void swap_rows16(double& x, double& y)
+{
+    const unsigned long long a = (unsigned long long)__double_as_longlong(x);
+    const unsigned long long b = (unsigned long long)__double_as_longlong(y);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)a, (unsigned)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(a >> 32), (unsigned)(b >> 32), false, false);
+    x = __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));
+    y = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));
+}
+
+// One window quarter: X[K][kk][jj] (K, kk, jj in 0..3) starts as the lane's
+// first-pass outputs a[4K + kk][4q + jj] (its lines j = 4q + jj) and ends as
+// a[4q + kk][4K + jj].  Stage 1 exchanges blocks between rows {0, 1} and
+// {2, 3}, stage 2 within the pairs (0, 1), (2, 3).
+__device__ __forceinline__ void transpose_quad(double (&X)[4][4][4])
+{
+#pragma unroll
+    for (int kk = 0; kk < 4; kk++)
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++) {
+            swap_rows32(X[0][kk][jj], X[2][kk][jj]);
+            swap_rows32(X[1][kk][jj], X[3][kk][jj]);
+        }
+#pragma unroll
+    for (int kk = 0; kk < 4; kk++)
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++) {
+            swap_rows16(X[0][kk][jj], X[1][kk][jj]);
+            swap_rows16(X[2][kk][jj], X[3][kk][jj]);
+        }
+}
+
+template <int BPP>
+struct D16Rows {
+    static constexpr int NW = (16 * BPP + 3) / 4 + 1;  // dwords of a line's 16 pixels, any alignment
+    uint32_t fv[4][NW];
+    uint32_t foff;      // 2 bits per line
+    uint32_t fast;      // bit per line
+    int x, y;
+    bool valid;
+};
+
+template <int BPP>
+__device__ __forceinline__ void fix_dense16_flat(const TileFixParams& tp, const double* lut,
+                                                 unsigned blk, unsigned nblk)
+{
+    constexpr int N = 16;
+    constexpr int HL = Geo<N, kSemLqr>::HL;
+    constexpr int NW = D16Rows<BPP>::NW;
+    const MapParams& p = tp.m;
+    DenseWalk<16> dw;
+    if (!dw.init(tp, blk, nblk)) return;               // uniform
+    const unsigned b0 = dw.b0, nb = dw.nb;
+    const int lane = threadIdx.x, q = lane >> 4, slot = lane & 15;
+    const uintptr_t pbase = reinterpret_cast<uintptr_t>(p.px);
+    const uint32_t base_off = (uint32_t)(pbase & 3u);
+    const unsigned nrec = base_off + (unsigned)((long long)(p.in_rows - 1) * p.rowstride) +
+                          (unsigned)(p.w * BPP);
+    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(pbase - base_off), (short)0, (int)nrec, (int)kBufFlags);
+    // liblqr luma (src/render.c:315, LQR_ER_LUMA) [liblqr, unverified]:
+    // grey v / 255; RGB (k_r r + k_g g) + k_b b through the pre-weighted tables
+    auto luma3 = [&](uint32_t c0, uint32_t c1, uint32_t c2) -> double {
+        if constexpr (BPP == 1) return lut[c0];
+        else return lut[c0] + lut[256 + c1] + lut[512 + c2];
+    };
+    // this lane's four lines: image rows y - HL + 4q + jj, pixels x - HL .. x - HL + 15
+    auto row_stage = [&](unsigned loc, int sx0, int ys, bool valid, D16Rows<BPP>& R) {
+        R.x = sx0 + (int)(loc & 63u);
+        R.y = ys + (int)(loc >> 6);
+        R.valid = valid;
+        const int gx0 = R.x - HL;
+        const bool inside = valid && gx0 >= 0 && gx0 + 16 <= p.w;
+        R.fast = 0;
+        R.foff = 0;
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++) {
+            const int gy = clampi(R.y - HL + 4 * q + jj, 0, p.h - 1);
+            const uint32_t s0 = base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
+                                (uint32_t)(gx0 * BPP);
+            const bool fast = inside && ((s0 + 16 * BPP - 1) | 3u) < nrec;
+            R.fast |= (uint32_t)fast << jj;
+            R.foff |= (s0 & 3u) << (2 * jj);
+            const uint32_t a = fast ? (s0 & ~3u) : 0x7ffffff0u;   // past num_records: zeros
+#pragma unroll
+            for (int j = 0; j < NW; j++)
+                R.fv[jj][j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * j), 0, 0);
+        }
+    };
+    // X[K][kk][jj] = luma of line jj, pixel 4K + kk (the first index)
+    auto convert = [&](const D16Rows<BPP>& R, double (&X)[4][4][4]) {
+        const int gx0 = R.x - HL;
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++) {
+            double lv[16];
+            // lanes without an entry decode their (zero) fetch like a fast line
+            if (((R.fast >> jj) & 1u) || !R.valid) {
+                const uint32_t fo = (R.foff >> (2 * jj)) & 3u;
+                uint32_t wd[NW - 1];
+#pragma unroll
+                for (int j = 0; j < NW - 1; j++) wd[j] = __builtin_amdgcn_alignbyte(R.fv[jj][j + 1], R.fv[jj][j], fo);
+#pragma unroll
+                for (int c = 0; c < 16; c++) {
+                    auto byte = [&](int b) { return (wd[b >> 2] >> (8 * (b & 3))) & 255u; };
+                    lv[c] = luma3(byte(c * BPP), BPP > 1 ? byte(c * BPP + 1) : 0u, BPP > 1 ? byte(c * BPP + 2) : 0u);
+                }
+            } else {
+                // clamped at the left / right border, or at the frame's last
+                // bytes (opaque copies: keep these addresses inside the branch)
+                int xs = gx0, yr = R.y - HL + 4 * q + jj;
+                asm volatile("" : "+v"(xs), "+v"(yr));
+                const int gy = clampi(yr, 0, p.h - 1);
+                const uint8_t* row = p.px + (long long)(gy - p.in_row0) * p.rowstride;
+#pragma unroll
+                for (int c = 0; c < 16; c++) {
+                    const uint8_t* q8 = row + (long long)clampi(xs + c, 0, p.w - 1) * BPP;
+                    lv[c] = luma3(q8[0], BPP > 1 ? q8[1] : 0u, BPP > 1 ? q8[2] : 0u);
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < 16; c++) X[c >> 2][c & 3][jj] = lv[c];
+        }
+    };
+
+    // batch-map entries of the next list16's batch b and of b + 1
+    uint4 infA = dw.info(b0), infB = b0 + 1 < nb ? dw.info(b0 + 1) : infA;
+    auto list16 = [&](unsigned b, unsigned& loc, int& sx0, int& ys, bool& valid) {
+        const uint4 A = infA, B = infB;
+        const unsigned bn = dw.next(b);
+        if (bn < nb) {                                 // uniform
+            infA = dw.info(bn);
+            infB = bn + 1 < nb ? dw.info(bn + 1) : infA;
+        }
+        dw.list(b, A, B, (unsigned)slot, loc, sx0, ys, valid);
+    };
+    unsigned locN = 0;
+    int sxN = 0, ysN = 0;
+    bool vN = false;
+    D16Rows<BPP> R;
+    {
+        unsigned loc0;
+        int sx, ys;
+        bool v;
+        list16(b0, loc0, sx, ys, v);
+        if (dw.next(b0) < nb) list16(dw.next(b0), locN, sxN, ysN, vN);
+        row_stage(loc0, sx, ys, v, R);
+    }
+    for (unsigned b = b0; b < nb; b = dw.next(b)) {    // uniform
+        double X[4][4][4];
+        convert(R, X);
+        const int x = R.x, y = R.y;
+        const bool v = R.valid;
+        // the next batch's loads reuse R's registers: not above the convert
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned bn = dw.next(b);
+        if (bn < nb) {                                 // uniform
+            row_stage(locN, sxN, ysN, vN, R);
+            if (dw.next(bn) < nb) list16(dw.next(bn), locN, sxN, ysN, vN);
+        }
+        // first pass: the lane's four lines along the first index
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++) {
+            double line[16];
+#pragma unroll
+            for (int c = 0; c < 16; c++) line[c] = X[c >> 2][c & 3][jj];
+            r64::step16(line, 1);
+#pragma unroll
+            for (int c = 0; c < 16; c++) X[c >> 2][c & 3][jj] = line[c];
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        transpose_quad(X);
+        // second pass: coefficient rows k1 = 4q + kk along the second index,
+        // and their maxima for the scan
+        double rmax[4], c01 = 0.0, c10 = 0.0, r0_2 = -1.0, r1_1 = -1.0;
+#pragma unroll
+        for (int kk = 0; kk < 4; kk++) {
+            double line[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) line[j] = X[j >> 2][kk][j & 3];
+            r64::step16(line, 1);
+            double m2 = -1.0;
+#pragma unroll
+            for (int k2 = 2; k2 < 16; k2++) m2 = fmax(m2, fabs(line[k2]));
+            if (kk == 0) {
+                c01 = fabs(line[1]);
+                r0_2 = m2;
+            } else if (kk == 1) {
+                c10 = fabs(line[0]);
+                r1_1 = fmax(m2, fabs(line[1]));
+            }
+            rmax[kk] = fmax(fmax(fabs(line[0]), fabs(line[1])), m2);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // indices past N = (1, 0) in the scan order: rows 1 (from k2 = 1), 2, 3 of
+        // quarter 0, every row of the others
+        double ma = q == 0 ? fmax(r1_1, fmax(rmax[2], rmax[3]))
+                           : fmax(fmax(rmax[0], rmax[1]), fmax(rmax[2], rmax[3]));
+        ma = fmax(ma, __shfl_xor(ma, 16));
+        ma = fmax(ma, __shfl_xor(ma, 32));
+        double m;
+        bool edge;
+        lastmax_decide(c01, c10, r0_2, ma, m, edge);
+        if (v && q == 0)
+            p.out[(long long)(y - p.y0) * p.out_stride + x] =
+                edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
+    }
+}
+
+#ifndef DCTE_DENSE16_MINW
+#define DCTE_DENSE16_MINW 2
+#endif
+template <int BPP>
+__global__ __launch_bounds__(64, DCTE_DENSE16_MINW) void dcte_fix_dense16(const TileFixParams tp)
+{
+    __shared__ double lut[BPP == 3 ? 3 * 256 : 256];
+    fill_luma_lut<BPP == 3>(lut, threadIdx.x);
+    wave_sync_lds();
+    fix_dense16_flat<BPP>(tp, lut, blockIdx.x, gridDim.x);
+}
+
 template <int BPP, int SEM>
 __global__ __launch_bounds__(64, DCTE_DENSE8_MINW) void dcte_fix_dense8(const TileFixParams tp)
 {
     constexpr bool kTab = SEM == kSemLqr && BPP == 3;
     __shared__ double lut[kTab ? 3 * 256 : 256];
-    if (blockIdx.x >= *tp.m.dirty_count) return;      // uniform
+    if (!DCTE_FIX_FLAT && blockIdx.x >= *tp.m.dirty_count) return;   // uniform
     fill_luma_lut<kTab>(lut, threadIdx.x);
     wave_sync_lds();
-    fix_dense8_run<BPP, SEM>(tp, lut, blockIdx.x, gridDim.x);
+    fix_dense8<BPP, SEM>(tp, lut, blockIdx.x, gridDim.x);
 }
 
 template <int N, int BPP, int SEM>
@@ -1161,31 +1738,42 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
     // 1.33 ms; at N = 16 the same costs +30 % (profiles/r02/fix_otf_ab.jsonl)
     constexpr bool kTab = DCTE_FIX_OTF_RGB && SEM == kSemLqr && BPP == 3 && N == 8;
     constexpr bool kOtf = DCTE_FIX_OTF && (BPP == 1 || kTab);
-    __shared__ double lut[kTab ? 3 * 256 : 256];
-    __shared__ double lum[kOtf ? 1 : LR * LW];         // fp64 luma of one band (+ halo), needed columns
+    // dense strips go to fix_dense8* / fix_dense16_flat (kDenseOwn): no band
+    // staging here, and the N = 16 RGB dense blocks want pre-weighted tables
+    constexpr bool kOwn = kDenseOwn<N, SEM>;
+    constexpr bool kTab16 = N == 16 && kOwn && BPP == 3;
+    __shared__ double lut[(kTab || kTab16) ? 3 * 256 : 256];
+    __shared__ double lum[(kOtf || kOwn) ? 1 : LR * LW];   // fp64 luma of one band (+ halo), needed columns
     __shared__ unsigned char mis[LR];                  // byte offset of each raw row's first pixel
-    __shared__ unsigned char colidx[kOtf ? 1 : LW];    // the needed luma columns, ascending
+    __shared__ unsigned char colidx[(kOtf || kOwn) ? 1 : LW];   // the needed luma columns, ascending
     // per group: N rows of N + 1 doubles, plus a pad that starts consecutive
     // groups 16 banks apart
     constexpr int WS = kGroup ? (N * (N + 1) + 7) / 8 * 8 + 8 : 1;
     // the band's raw rows and the groups' window buffers: one region when raw
     // is read only by the luma conversion (the windows only after it)
-    // (N = 8 with dcte_fix_dense8 runs no dense band here: no raw band)
-    constexpr int RAW_D = (N == 8 && DCTE_FIX_LANES) ? 0 : (LR * PDW + 1) / 2, WIN_D = (kGroup ? PPW : 1) * WS;
+    // (no dense band here when the dense strips have a kernel of their own)
+    constexpr int RAW_D = kOwn ? 0 : (LR * PDW + 1) / 2, WIN_D = (kGroup ? PPW : 1) * WS;
     constexpr int RW_D = kOtf ? RAW_D + WIN_D : (RAW_D > WIN_D ? RAW_D : WIN_D);
     __shared__ __attribute__((aligned(16))) double rw_lds[RW_D];
     uint32_t* const raw = reinterpret_cast<uint32_t*>(rw_lds);
     double (*const win)[WS] = reinterpret_cast<double (*)[WS]>(rw_lds + (kOtf ? RAW_D : 0));
     const MapParams& p = tp.m;
     const unsigned ndirty = *p.dirty_count;
-    if constexpr (N == 8 && DCTE_FIX_LANES && DCTE_FIX_MERGE) {
+    if constexpr (kOwn && DCTE_FIX_MERGE) {
         // one launch for both: blocks past tp.sparse_blocks walk the dense strips
         if (blockIdx.x >= (unsigned)tp.sparse_blocks) {
             const unsigned blk = blockIdx.x - (unsigned)tp.sparse_blocks;
-            if (blk >= ndirty) return;                 // uniform
-            fill_luma_lut<kTab>(lut, threadIdx.x);
-            wave_sync_lds();
-            fix_dense8_run<BPP, SEM>(tp, lut, blk, gridDim.x - (unsigned)tp.sparse_blocks);
+            const unsigned nblk = gridDim.x - (unsigned)tp.sparse_blocks;
+            if constexpr (N == 8) {
+                if (!DCTE_FIX_FLAT && blk >= ndirty) return;   // uniform
+                fill_luma_lut<kTab>(lut, threadIdx.x);
+                wave_sync_lds();
+                fix_dense8<BPP, SEM>(tp, lut, blk, nblk);
+            } else {
+                fill_luma_lut<kTab16>(lut, threadIdx.x);
+                wave_sync_lds();
+                fix_dense16_flat<BPP>(tp, lut, blk, nblk);
+            }
             return;
         }
     }
@@ -1422,7 +2010,7 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
         }
 
         // the batch's dense strips, one at a time (N = 8: dcte_fix_dense8)
-        uint64_t dense_mask = (N == 8 && DCTE_FIX_LANES) ? 0ull : __ballot(!sparse && sl == 0);
+        uint64_t dense_mask = kOwn ? 0ull : __ballot(!sparse && sl == 0);
         while (dense_mask) {                                              // uniform
             const int leader = __builtin_ctzll(dense_mask);             // lane 0 of its group
             dense_mask &= dense_mask - 1;
@@ -1819,21 +2407,32 @@ static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
         if (dev >= 0 && dev < kMaxDevices) cache[dev].store(resident, std::memory_order_relaxed);
     }
     const int blocks = nstrips < resident ? nstrips : resident;
-    if constexpr (N == 8 && DCTE_FIX_LANES) {
+    if constexpr (kDenseOwn<N, SEM>) {
+        // the dense strips' walk: its own kernel (occupancy from its
+        // registers), or extra blocks of the same launch (DCTE_FIX_MERGE)
+        auto dense_kernel = [] {
+            if constexpr (N == 8) return dcte_fix_dense8<BPP, SEM>;
+            else return dcte_fix_dense16<BPP>;
+        }();
         static std::atomic<int> dcache[kMaxDevices];
         int dres = dev >= 0 && dev < kMaxDevices ? dcache[dev].load(std::memory_order_relaxed) : 0;
         if (!dres) {
             int cus = 0, per_cu = 0;
             if (dev >= 0 &&
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dcte_fix_dense8<BPP, SEM>, 64, 0) ==
-                    hipSuccess && cus > 0 && per_cu > 0)
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dense_kernel, 64, 0) == hipSuccess &&
+                cus > 0 && per_cu > 0)
                 dres = cus * per_cu;
             else
                 dres = 2048;
             if (dev >= 0 && dev < kMaxDevices) dcache[dev].store(dres, std::memory_order_relaxed);
         }
-        const int dblocks = nstrips < dres ? nstrips : dres;
+        // flat list: up to one wave per batch the lists could hold; per-strip
+        // walk (N = 8, DCTE_FIX_FLAT=0): one per strip
+        const long long most = kDenseFlat<N, SEM>
+                                   ? ((long long)nstrips * 64 * p.m.tile_h + kDenseBatch<N> - 1) / kDenseBatch<N>
+                                   : nstrips;
+        const int dblocks = most < dres ? (int)most : dres;
         if constexpr (DCTE_FIX_MERGE) {
             TileFixParams q = p;
             q.sparse_blocks = blocks;
@@ -1843,7 +2442,7 @@ static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
         hipLaunchKernelGGL((dcte_fix_strips<N, BPP, SEM>), dim3(blocks), dim3(64), 0, s, p);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((dcte_fix_dense8<BPP, SEM>), dim3(dblocks), dim3(64), 0, s, p);
+        hipLaunchKernelGGL(dense_kernel, dim3(dblocks), dim3(64), 0, s, p);
         return hipGetLastError();
     }
     hipLaunchKernelGGL((dcte_fix_strips<N, BPP, SEM>), dim3(blocks), dim3(64), 0, s, p);

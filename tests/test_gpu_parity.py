@@ -263,6 +263,30 @@ def test_tie_dense_full_size(ctx):
         torch.cuda.empty_cache()
 
 
+def test_tie_dense_full_size_n16(ctx):
+    """N = 16 (configs[4]'s block size, 8192^2) on line art: 4.3 % of the
+    pixels flagged, their dense strips refined four lanes per pixel with the
+    window transposed across the wave's rows (fix_dense16_flat) -- RGB at the
+    config's size and grey at 4096^2, every pixel against the oracle, 0 class
+    flips."""
+    torch = _torch()
+    for S, rgb in ((8192, True), (4096, False)):
+        yy, xx = np.ogrid[0:S, 0:S]
+        ink = (yy % 23 == 0) | (xx % 31 == 0) | ((xx + 2 * yy) % 97 == 0)
+        img = np.where(ink, 0, 255).astype(np.uint8)
+        del ink
+        if rgb:
+            img = np.repeat(img[..., None], 3, -1)
+        out = torch.from_numpy(ctx.energy_map(img, 16, 0.3, 0.7)).cuda()
+        refined = ctx.last_refined
+        ref = O.energy_map(img, 16, 0.3, 0.7, nthreads=NTHREADS)
+        st = _compare_full(out, ref, 0.3, 0.7, f"lineart {'rgb' if rgb else 'grey'} {S}^2 N=16")
+        print("lineart", S, "rgb" if rgb else "grey", "refined", refined, st)
+        assert refined > 100000
+        del out, ref
+        torch.cuda.empty_cache()
+
+
 def test_ties_are_refined_to_reference(ctx):
     """Images full of exact edge/texture ties (isolated pixels on flat ground)
     match the reference bit-exactly where the class is decided by rounding."""
