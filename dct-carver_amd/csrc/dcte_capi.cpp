@@ -323,10 +323,10 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     if (rc) return rc;
     rc = ensure_tiles(ctx, f, ntiles);
     if (rc) return rc;
-    // the dense refinement's batch map (N = 8, and N = 16 liblqr): one uint4
-    // per batch of 64 (16) entries the lists can hold
-    if (n == 8 || (n == 16 && sem == DCTE_LQR)) {
-        rc = ensure_buf(ctx, &f->d_batch, &f->bcap, (list_len / (n == 8 ? 64 : 16) + 1) * 16);
+    // the dense refinement's batch map (N = 16 liblqr; N = 8 in flat-walk
+    // builds): one uint4 per batch the lists can hold
+    if (const int epb = dcte::dense_batch_entries(n, sem)) {
+        rc = ensure_buf(ctx, &f->d_batch, &f->bcap, (list_len / (size_t)epb + 1) * 16);
         if (rc) return rc;
     }
 

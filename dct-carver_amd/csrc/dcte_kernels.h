@@ -170,5 +170,6 @@ int map_default_tile_h(int n);
 int map_tiles_x(int n, int w, bool wide = false);   // map grid (tiles) of a launch
 int map_tiles_y(int n, int rows, int tile_h);
 int map_strips_per_tile(int n, bool wide = false);
+int dense_batch_entries(int n, int sem);   // entries per dense refinement batch (0: no flat list)
 
 }  // namespace dcte

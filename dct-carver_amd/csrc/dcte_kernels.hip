@@ -93,7 +93,13 @@ constexpr unsigned kBufFlags = 0x00020000u;  // gfx9 raw buffer dword3
 #define DCTE_FIX_LANES 1 // dense strips at N = 8: one lane per pixel, window in registers
 #endif
 #ifndef DCTE_FIX_FLAT
-#define DCTE_FIX_FLAT 1  // ... taken from one flat list of all dense entries, 64 at a time, pipelined
+// ... taken from one flat list of all dense entries, 64 at a time, pipelined
+// (fix_dense8_flat).  Off: one wave walks whole strips (fix_dense8_run),
+// which keeps the window rows of a strip in the wave's L1 and the grey walk
+// at 162 VGPRs (3 waves per SIMD).  A/B at 16384^2 (profiles/r03/dense_flat_ab.jsonl):
+// the flat walk wins where dense strips are short (dots -20 %, text -25 %)
+// and loses where they are long (line art +8 %, the 8-px grid +16..22 %)
+#define DCTE_FIX_FLAT 0
 #endif
 template <int N>
 constexpr unsigned kFixDirect = N == 16 ? 32u : 128u;
@@ -1508,6 +1514,9 @@ __device__ __forceinline__ void transpose_quad(double (&X)[4][4][4])
         }
 }
 
+#ifndef DCTE_DENSE16_PF
+#define DCTE_DENSE16_PF 1    // a batch's window lines load during the previous batch
+#endif
 template <int BPP>
 struct D16Rows {
     static constexpr int NW = (16 * BPP + 3) / 4 + 1;  // dwords of a line's 16 pixels, any alignment
@@ -1614,6 +1623,8 @@ __device__ __forceinline__ void fix_dense16_flat(const TileFixParams& tp, const 
     unsigned locN = 0;
     int sxN = 0, ysN = 0;
     bool vN = false;
+    // lines one batch ahead (DCTE_DENSE16_PF), or loaded at their batch
+    constexpr bool kPF = DCTE_DENSE16_PF;
     D16Rows<BPP> R;
     {
         unsigned loc0;
@@ -1621,10 +1632,15 @@ __device__ __forceinline__ void fix_dense16_flat(const TileFixParams& tp, const 
         bool v;
         list16(b0, loc0, sx, ys, v);
         if (dw.next(b0) < nb) list16(dw.next(b0), locN, sxN, ysN, vN);
-        row_stage(loc0, sx, ys, v, R);
+        if constexpr (kPF) row_stage(loc0, sx, ys, v, R);
+        else { R.x = sx; R.y = ys; R.valid = v; R.fast = loc0; }   // parked: batch b0's list word
     }
     for (unsigned b = b0; b < nb; b = dw.next(b)) {    // uniform
         double X[4][4][4];
+        if constexpr (!kPF) {
+            const unsigned loc = R.fast;
+            row_stage(loc, R.x, R.y, R.valid, R);
+        }
         convert(R, X);
         const int x = R.x, y = R.y;
         const bool v = R.valid;
@@ -1632,7 +1648,14 @@ __device__ __forceinline__ void fix_dense16_flat(const TileFixParams& tp, const 
         __builtin_amdgcn_sched_barrier(0);
         const unsigned bn = dw.next(b);
         if (bn < nb) {                                 // uniform
-            row_stage(locN, sxN, ysN, vN, R);
+            if constexpr (kPF) {
+                row_stage(locN, sxN, ysN, vN, R);
+            } else {
+                R.x = sxN;
+                R.y = ysN;
+                R.valid = vN;
+                R.fast = locN;
+            }
             if (dw.next(bn) < nb) list16(dw.next(bn), locN, sxN, ysN, vN);
         }
         // first pass: the lane's four lines along the first index
@@ -2473,6 +2496,13 @@ hipError_t launch_fix_tiles(int n, int bpp, int sem, const TileFixParams& p, hip
     case 16: return launch_fix_tiles_n<16>(bpp, sem, p, s);
     default: return hipErrorInvalidValue;
     }
+}
+
+int dense_batch_entries(int n, int sem)
+{
+    if (n == 8) return kDenseFlat<8, kSemLqr> ? (int)kDenseBatch<8> : 0;
+    if (n == 16 && sem == kSemLqr) return kDenseFlat<16, kSemLqr> ? (int)kDenseBatch<16> : 0;
+    return 0;
 }
 
 hipError_t launch_windows(const WinParams& p, hipStream_t s)
