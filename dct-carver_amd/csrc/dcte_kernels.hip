@@ -1231,7 +1231,7 @@ struct D8Rows {
 // strip holds more than kFixDirect >= EPB entries), the second one is the
 // next slot of dense_list.
 #ifndef DCTE_DENSE_CHUNK
-#define DCTE_DENSE_CHUNK 8      // consecutive refinement batches per wave before it strides on
+#define DCTE_DENSE_CHUNK 1      // consecutive refinement batches per wave before it strides on (N = 16: 1 -4 %, 8 +0, 32 +7..14 % vs 8, profiles/r03/dense16_ab.jsonl)
 #endif
 template <int EPB>
 struct DenseWalk {
