@@ -1877,7 +1877,12 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
     // strips follow one at a time, each walked by the whole wave.
     constexpr int GL = 64 / SB;
     const int sgi = lane / GL, sl = lane % GL;
-    for (unsigned k0 = blockIdx.x * SB; k0 < ndirty; k0 += gridDim.x * SB) {   // uniform
+    // the sparse walk's blocks: in a merged launch only the first
+    // tp.sparse_blocks (the rest walk the dense strips), so they stride by
+    // that many -- striding by gridDim.x skipped every strip batch past
+    // sparse_blocks * SB in launches with more dirty strips than that
+    const unsigned nsparse = (kOwn && DCTE_FIX_MERGE) ? (unsigned)tp.sparse_blocks : gridDim.x;
+    for (unsigned k0 = blockIdx.x * SB; k0 < ndirty; k0 += nsparse * SB) {   // uniform
         const unsigned kk = k0 + sgi;
         unsigned my_strip = 0, my_cnt = 0;
         if (kk < ndirty) {

@@ -263,6 +263,28 @@ def test_tie_dense_full_size(ctx):
         torch.cuda.empty_cache()
 
 
+def test_tie_dense_one_launch(ctx):
+    """A whole 16384^2 frame in ONE device launch (the host entry point maps
+    1024-row chunks): text-like blocks dirty almost every 64-column strip, more
+    strips than the refinement launch's sparse walkers take in one stride,
+    and hold sparse and dense strips side by side.  Every pixel against the
+    oracle, at N = 8 and (8192^2) N = 16, 0 class flips."""
+    torch = _torch()
+    for S, n in ((16384, 8), (8192, 16)):
+        rng = np.random.default_rng(31 + n)
+        blk = rng.random((S // 4 + 1, S // 4 + 1)) < 0.3
+        img = np.where(np.repeat(np.repeat(blk, 4, 0), 4, 1)[:S, :S], 0, 255).astype(np.uint8)
+        del blk
+        out = torch.empty((S, S), dtype=torch.float32, device="cuda")
+        ctx.energy_map_tensor(torch.from_numpy(img).cuda(), out, n, 0.3, 0.7)
+        torch.cuda.synchronize()
+        ref = O.energy_map(img, n, 0.3, 0.7, nthreads=NTHREADS)
+        st = _compare_full(out, ref, 0.3, 0.7, f"text {S}^2 N={n} one launch")
+        print("text one launch", S, n, st)
+        del out, ref
+        torch.cuda.empty_cache()
+
+
 def test_tie_dense_full_size_n16(ctx):
     """N = 16 (configs[4]'s block size, 8192^2) on line art: 4.3 % of the
     pixels flagged, their dense strips refined four lanes per pixel with the
