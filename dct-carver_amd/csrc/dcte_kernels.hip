@@ -101,8 +101,11 @@ constexpr unsigned kBufFlags = 0x00020000u;  // gfx9 raw buffer dword3
 // and loses where they are long (line art +8 %, the 8-px grid +16..22 %)
 #define DCTE_FIX_FLAT 0
 #endif
+#ifndef DCTE_FIX_DIRECT8
+#define DCTE_FIX_DIRECT8 16u    // N <= 8: most flagged pixels a strip may hold and still be sparse (128 before: dots +47 %, text +4 %; profiles/r03/fix_direct_ab.jsonl)
+#endif
 template <int N>
-constexpr unsigned kFixDirect = N == 16 ? 32u : 128u;
+constexpr unsigned kFixDirect = N == 16 ? 32u : (unsigned)DCTE_FIX_DIRECT8;
 #ifndef DCTE_FIX_QUAD16
 #define DCTE_FIX_QUAD16 1 // dense strips at N = 16 (liblqr): four lanes per pixel, window in registers
 #endif
@@ -118,6 +121,10 @@ constexpr bool kDenseFlat = (N == 8 && DCTE_FIX_LANES && DCTE_FIX_FLAT) || (N ==
 // a quad of lanes at N = 16
 template <int N>
 constexpr unsigned kDenseBatch = N == 8 ? 64u : 16u;
+// the flat walk's batches span at most two strips only if a dense strip
+// holds more entries than a batch
+static_assert(!kDenseFlat<8, kSemLqr> || kFixDirect<8> >= kDenseBatch<8>, "DCTE_FIX_FLAT needs DCTE_FIX_DIRECT8 >= 64");
+static_assert(!kDenseFlat<16, kSemLqr> || kFixDirect<16> >= kDenseBatch<16>, "N = 16 dense batches");
 
 // SEM = kSemLqr    : liblqr callback window, offsets -(N/2-1)..N/2
 //                    (src/render.c:146-152), liblqr luma (dcte_luma.h)
@@ -944,9 +951,10 @@ __global__ __launch_bounds__(kFixThreads) void dcte_fix(const FixParams p)
 // One lane per pixel for N <= 4 (the window in registers), one N-lane group
 // per pixel for N = 8, 16 (the window in LDS).
 // Strips with at most kFixDirect<N> flagged pixels take the direct path: N <= 8
-// at 128 (dots on flat ground, 0.37 % flagged at 16384^2: 0.31 ms vs 0.58 at
-// 32; line art unchanged, worse from 256), N = 16 at 32
-// (profiles/r02/fix_direct.jsonl).
+// at 16 since the lane-per-pixel dense walk (dots on flat ground, 0.37 %
+// flagged at 16384^2: 0.17 ms vs 0.24 at 128, 0.16 at 8 where text loses
+// 10 %; profiles/r03/fix_direct_ab.jsonl -- with the band path of r02 the
+// best was 128), N = 16 at 32 (profiles/r02/fix_direct.jsonl).
 #ifndef DCTE_FIX_ALIGNED
 #define DCTE_FIX_ALIGNED 1  // dense strips read the staged raw bytes as aligned dwords
 #endif
