@@ -47,7 +47,8 @@ struct MapParams {
     unsigned long long* dense_ctr;
     unsigned long long* dense_next;
     uint2* dense_list;
-    // and per refinement batch b (kDenseBatch entries of the flat list,
+    // and (written by dcte_dense_index, between the map launch and its
+    // refinement) per refinement batch b (kDenseBatch entries of the flat list,
     // 64 at N = 8, 16 at N = 16) the dense strip holding its first entry:
     // {its first column, its tile's first output row, strip, offset of its
     // first entry in the flat list}

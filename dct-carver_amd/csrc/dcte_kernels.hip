@@ -204,8 +204,6 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
     // refinement lists per 64-column strip (one wave's columns; N = 16: the tile)
     constexpr int SPT = S == 1 ? TW / 64 : 1;        // strips per tile
     __shared__ unsigned nflag[SPT];                  // pixels each strip flagged
-    __shared__ uint4 dense_sh[kDenseFlat<N, SEM> ? SPT : 1];   // dense strips' batch-map entries
-    __shared__ unsigned dense_cnt[kDenseFlat<N, SEM> ? SPT : 1];
 
     const int tx = threadIdx.x;
     const int lane_p = (S == 4) ? (tx >> 6) : 0;     // N = 16: wave index = k1 class
@@ -626,8 +624,6 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
     }
     __syncthreads();
     if (tx < SPT) {
-        uint4 di = make_uint4(0u, 0u, 0u, 0u);
-        unsigned dcnt = 0;                             // 0: not a dense strip
         const unsigned cnt = nflag[tx];
         if (cnt) {
             const unsigned st = strip - sc + tx;
@@ -638,31 +634,8 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
                 const unsigned slot = (unsigned)(r >> 32), off = (unsigned)r;
                 // a launch holds gridDim.x * gridDim.y * SPT strips (the guard only
                 // matters if the counter did not start at zero)
-                if (slot < gridDim.x * gridDim.y * SPT) {
-                    p.dense_list[slot] = make_uint2(st, off);
-                    di = make_uint4((unsigned)(x0 + 64 * tx), (unsigned)ys, st, off);
-                    dcnt = cnt;
-                }
+                if (slot < gridDim.x * gridDim.y * SPT) p.dense_list[slot] = make_uint2(st, off);
             }
-        }
-        if constexpr (kDenseFlat<N, SEM>) {
-            dense_sh[tx] = di;
-            dense_cnt[tx] = dcnt;
-        }
-    }
-    if constexpr (kDenseFlat<N, SEM>) {
-        // the batch map: every refinement batch (kDenseBatch<N> entries of the
-        // flat list) whose first entry lies in one of this workgroup's dense
-        // strips points at that strip, so a wave finds any batch in one load
-        __syncthreads();
-        constexpr unsigned EPB = kDenseBatch<N>;
-#pragma unroll
-        for (int k = 0; k < SPT; k++) {
-            const uint4 di = dense_sh[k];
-            const unsigned cnt = dense_cnt[k];
-            if (cnt == 0u) continue;                   // uniform
-            const unsigned first = (di.w + EPB - 1u) / EPB, last = (di.w + cnt - 1u) / EPB;
-            for (unsigned b = first + (unsigned)tx; b <= last; b += (unsigned)kThreads) p.dense_batch[b] = di;
         }
     }
 #if DCTE_TSTAMP
@@ -1298,6 +1271,28 @@ struct DenseWalk {
         loc = tp->m.fix_list[valid ? idx : A.z * per_strip];
     }
 };
+
+// The batch map of a flat dense list, between the map launch and its
+// refinement (a pass of its own: written from the map kernel's tail it cost
+// the N = 16 map kernel a spilled register): wave k takes dense slot k and
+// writes, for every batch of EPB entries whose first entry lies in that
+// strip, {first column, first output row, strip, offset}.
+template <int EPB>
+__global__ __launch_bounds__(256) void dcte_dense_index(const TileFixParams tp)
+{
+    const MapParams& p = tp.m;
+    const unsigned slot = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const unsigned nd = (unsigned)(*p.dense_ctr >> 32);
+    const unsigned spt = (unsigned)tp.tile_w / 64u;
+    const unsigned nstrips = (unsigned)tp.tiles_x * spt * (unsigned)((p.y1 - p.y0 + p.tile_h - 1) / p.tile_h);
+    if (slot >= nd || nd > nstrips) return;            // uniform per wave
+    const uint2 v = p.dense_list[slot];
+    const unsigned strip = v.x, off = v.y, cnt = p.tile_count[strip], tile = strip / spt;
+    const uint4 di = make_uint4((unsigned)((int)(tile % (unsigned)tp.tiles_x) * tp.tile_w + 64 * (int)(strip % spt)),
+                                (unsigned)(p.y0 + (int)(tile / (unsigned)tp.tiles_x) * p.tile_h), strip, off);
+    const unsigned first = (off + EPB - 1u) / EPB, last = (off + cnt - 1u) / EPB;
+    for (unsigned b = first + lane; b <= last; b += 64u) p.dense_batch[b] = di;
+}
 
 template <int BPP, int SEM>
 __device__ __forceinline__ void fix_dense8_flat(const TileFixParams& tp, const double* lut,
@@ -2443,6 +2438,11 @@ static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
         if (dev >= 0 && dev < kMaxDevices) cache[dev].store(resident, std::memory_order_relaxed);
     }
     const int blocks = nstrips < resident ? nstrips : resident;
+    if constexpr (kDenseFlat<N, SEM>) {
+        // the flat list's batch map first (one wave per possible dense strip)
+        hipLaunchKernelGGL((dcte_dense_index<kDenseBatch<N>>), dim3((nstrips + 3) / 4), dim3(256), 0, s, p);
+        if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    }
     if constexpr (kDenseOwn<N, SEM>) {
         // the dense strips' walk: its own kernel (occupancy from its
         // registers), or extra blocks of the same launch (DCTE_FIX_MERGE)
