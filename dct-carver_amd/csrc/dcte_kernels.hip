@@ -121,6 +121,27 @@ constexpr bool kDenseFlat = (N == 8 && DCTE_FIX_LANES && DCTE_FIX_FLAT) || (N ==
 // a quad of lanes at N = 16
 template <int N>
 constexpr unsigned kDenseBatch = N == 8 ? 64u : 16u;
+#ifndef DCTE_FIX_GATHER
+#define DCTE_FIX_GATHER 0       // N = 8: strips of at most DCTE_GATHER_MAX flags pooled into full 64-pixel batches (measured slower: profiles/r03/gather_ab.jsonl)
+#endif
+#ifndef DCTE_GATHER_MAX
+#define DCTE_GATHER_MAX 128u
+#endif
+// N = 8 with the gather walk (fix_gather8): the flat list holds the SMALL
+// strips (1 .. kGatherMax flags), pooled 64 pixels per batch whatever their
+// strips; longer strips keep the per-strip walk and nothing is left sparse
+template <int N, int SEM>
+constexpr bool kGather = N == 8 && DCTE_FIX_LANES && !DCTE_FIX_FLAT && DCTE_FIX_GATHER;
+constexpr unsigned kGatherMax = DCTE_GATHER_MAX;
+// the map kernel fills the flat list (dense strips, or gathered small ones)
+template <int N, int SEM>
+constexpr bool kFlatList = kDenseFlat<N, SEM> || kGather<N, SEM>;
+// most flags a strip may hold and still go to dcte_fix_strips' sparse walk
+template <int N, int SEM>
+constexpr unsigned kSparseMax = kGather<N, SEM> ? 0u : kFixDirect<N>;
+// fewest flags (exclusive) of a strip the per-strip dense walk takes
+template <int N, int SEM>
+constexpr unsigned kDenseMin = kGather<N, SEM> ? kGatherMax : kFixDirect<N>;
 // the flat walk's batches span at most two strips only if a dense strip
 // holds more entries than a batch
 static_assert(!kDenseFlat<8, kSemLqr> || kFixDirect<8> >= kDenseBatch<8>, "DCTE_FIX_FLAT needs DCTE_FIX_DIRECT8 >= 64");
@@ -629,7 +650,7 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
             const unsigned st = strip - sc + tx;
             p.tile_count[st] = cnt;
             p.dirty_list[atomicAdd(p.dirty_count, 1u)] = st;
-            if (kDenseFlat<N, SEM> && cnt > kFixDirect<N>) {
+            if ((kDenseFlat<N, SEM> && cnt > kFixDirect<N>) || (kGather<N, SEM> && cnt <= kGatherMax)) {
                 const unsigned long long r = atomicAdd(p.dense_ctr, (1ull << 32) | cnt);
                 const unsigned slot = (unsigned)(r >> 32), off = (unsigned)r;
                 // a launch holds gridDim.x * gridDim.y * SPT strips (the guard only
@@ -1089,7 +1110,7 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
     for (unsigned k = blk; k < ndirty; k += nblk) {   // uniform
         const unsigned strip = p.dirty_list[k];
         const unsigned cnt = p.tile_count[strip];
-        if (cnt <= kFixDirect<N>) continue;            // sparse: dcte_fix_strips
+        if (cnt <= kDenseMin<N, SEM>) continue;        // sparse (dcte_fix_strips) or gathered (fix_gather8)
         const unsigned tile = strip / spt;
         const int bx = (int)(tile % (unsigned)tp.tiles_x), by = (int)(tile / (unsigned)tp.tiles_x);
         const int sx0 = bx * tp.tile_w + 64 * (int)(strip % spt);
@@ -1277,7 +1298,7 @@ struct DenseWalk {
 // the N = 16 map kernel a spilled register): wave k takes dense slot k and
 // writes, for every batch of EPB entries whose first entry lies in that
 // strip, {first column, first output row, strip, offset}.
-template <int EPB>
+template <int EPB, bool SLOT>
 __global__ __launch_bounds__(256) void dcte_dense_index(const TileFixParams tp)
 {
     const MapParams& p = tp.m;
@@ -1291,30 +1312,42 @@ __global__ __launch_bounds__(256) void dcte_dense_index(const TileFixParams tp)
     const uint4 di = make_uint4((unsigned)((int)(tile % (unsigned)tp.tiles_x) * tp.tile_w + 64 * (int)(strip % spt)),
                                 (unsigned)(p.y0 + (int)(tile / (unsigned)tp.tiles_x) * p.tile_h), strip, off);
     const unsigned first = (off + EPB - 1u) / EPB, last = (off + cnt - 1u) / EPB;
-    for (unsigned b = first + lane; b <= last; b += 64u) p.dense_batch[b] = di;
+    if constexpr (SLOT) {                              // gather walk: the slot alone
+        for (unsigned b = first + lane; b <= last; b += 64u) reinterpret_cast<unsigned*>(p.dense_batch)[b] = slot;
+    } else {
+        for (unsigned b = first + lane; b <= last; b += 64u) p.dense_batch[b] = di;
+    }
 }
 
+// Window I/O of the lane-per-pixel N = 8 walks (fix_dense8_flat,
+// fix_gather8): a pixel's eight image rows as whole dwords through the frame's
+// buffer resource (per-pixel reads where the window is clamped at the left /
+// right border or reaches the frame's last bytes), converted to the
+// reference's fp64 luma (liblqr LQR_ER_LUMA through the LDS tables,
+// src/render.c:315 [liblqr, unverified], in the reference's order ((k_r r +
+// k_g g) + k_b b); preview: RGB2LUMINANCE) in the window layout refine_regs
+// takes (liblqr data[dx][dy], preview data[dy][dx]).
 template <int BPP, int SEM>
-__device__ __forceinline__ void fix_dense8_flat(const TileFixParams& tp, const double* lut,
-                                                unsigned blk, unsigned nblk)
-{
-    constexpr int N = 8;
-    constexpr int HL = Geo<N, SEM>::HL;
-    constexpr int NW = D8Rows<BPP>::NW;
-    const MapParams& p = tp.m;
-    DenseWalk<64> dw;
-    if (!dw.init(tp, blk, nblk)) return;               // uniform
-    const unsigned b0 = dw.b0, nb = dw.nb;
-    const int lane = threadIdx.x;
-    const uintptr_t pbase = reinterpret_cast<uintptr_t>(p.px);
-    const uint32_t base_off = (uint32_t)(pbase & 3u);
-    const unsigned nrec = base_off + (unsigned)((long long)(p.in_rows - 1) * p.rowstride) +
-                          (unsigned)(p.w * BPP);
-    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(pbase - base_off), (short)0, (int)nrec, (int)kBufFlags);
-    // liblqr luma (src/render.c:315, LQR_ER_LUMA) [liblqr, unverified] in the
-    // reference's order ((k_r r + k_g g) + k_b b); preview: RGB2LUMINANCE
-    auto luma3 = [&](uint32_t c0, uint32_t c1, uint32_t c2) -> double {
+struct Win8Io {
+    static constexpr int HL = Geo<8, SEM>::HL;
+    static constexpr int NW = D8Rows<BPP>::NW;
+    const MapParams& p;
+    const double* lut;
+    uint32_t base_off;
+    unsigned nrec;
+    __amdgpu_buffer_rsrc_t rsrc;
+
+    __device__ __forceinline__ Win8Io(const MapParams& mp, const double* l) : p(mp), lut(l)
+    {
+        const uintptr_t pbase = reinterpret_cast<uintptr_t>(p.px);
+        base_off = (uint32_t)(pbase & 3u);
+        nrec = base_off + (unsigned)((long long)(p.in_rows - 1) * p.rowstride) + (unsigned)(p.w * BPP);
+        rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(pbase - base_off), (short)0, (int)nrec,
+                                                 (int)kBufFlags);
+    }
+
+    __device__ __forceinline__ double luma3(uint32_t c0, uint32_t c1, uint32_t c2) const
+    {
         if constexpr (DCTE_DENSE8_PROBE == 1) return (double)(c0 + c1 + c2);
         if constexpr (SEM == kSemLqr) {
             if constexpr (BPP == 1) return lut[c0];
@@ -1322,22 +1355,11 @@ __device__ __forceinline__ void fix_dense8_flat(const TileFixParams& tp, const d
         } else {
             return (double)preview_luma(c0, c1, c2, BPP);
         }
-    };
-    // batch-map entries of the next list_stage's batch b and of b + 1
-    uint4 infA = dw.info(b0), infB = b0 + 1 < nb ? dw.info(b0 + 1) : infA;
-    auto list_stage = [&](unsigned b, unsigned& loc, int& sx0, int& ys, bool& valid) {
-        const uint4 A = infA, B = infB;
-        const unsigned bn = dw.next(b);
-        if (bn < nb) {                                 // uniform
-            infA = dw.info(bn);
-            infB = bn + 1 < nb ? dw.info(bn + 1) : infA;
-        }
-        dw.list(b, A, B, (unsigned)lane, loc, sx0, ys, valid);
-    };
-    // batch's window rows: the eight image rows as whole dwords through the
-    // frame's buffer resource (per-pixel reads where the window is clamped at
-    // the left / right border or reaches the frame's last bytes)
-    auto row_stage = [&](unsigned loc, int sx0, int ys, bool valid, D8Rows<BPP>& R) {
+    }
+
+    // the window rows of list word loc of the strip at (sx0, ys) into R
+    __device__ __forceinline__ void rows(unsigned loc, int sx0, int ys, bool valid, D8Rows<BPP>& R) const
+    {
         R.x = sx0 + (int)(loc & 63u);
         R.y = ys + (int)(loc >> 6);
         R.valid = valid;
@@ -1359,8 +1381,10 @@ __device__ __forceinline__ void fix_dense8_flat(const TileFixParams& tp, const d
                 R.fv[rr][j] = DCTE_DENSE8_PROBE == 3 ? ((a & 4u) ? 0xffffffffu : 0u)
                                                      : __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * j), 0, 0);
         }
-    };
-    auto convert = [&](const D8Rows<BPP>& R, double (&d)[64]) {
+    }
+
+    __device__ __forceinline__ void convert(const D8Rows<BPP>& R, double (&d)[64]) const
+    {
         const int gx0 = R.x - HL;
 #pragma unroll
         for (int r = 0; r < 8; r++) {
@@ -1393,7 +1417,32 @@ __device__ __forceinline__ void fix_dense8_flat(const TileFixParams& tp, const d
 #pragma unroll
             for (int c = 0; c < 8; c++) d[SEM == kSemLqr ? c * 8 + r : r * 8 + c] = lv[c];
         }
+    }
+};
+
+template <int BPP, int SEM>
+__device__ __forceinline__ void fix_dense8_flat(const TileFixParams& tp, const double* lut,
+                                                unsigned blk, unsigned nblk)
+{
+    const MapParams& p = tp.m;
+    DenseWalk<64> dw;
+    if (!dw.init(tp, blk, nblk)) return;               // uniform
+    const unsigned b0 = dw.b0, nb = dw.nb;
+    const int lane = threadIdx.x;
+    const Win8Io<BPP, SEM> io(p, lut);
+    // batch-map entries of the next list_stage's batch b and of b + 1
+    uint4 infA = dw.info(b0), infB = b0 + 1 < nb ? dw.info(b0 + 1) : infA;
+    auto list_stage = [&](unsigned b, unsigned& loc, int& sx0, int& ys, bool& valid) {
+        const uint4 A = infA, B = infB;
+        const unsigned bn = dw.next(b);
+        if (bn < nb) {                                 // uniform
+            infA = dw.info(bn);
+            infB = bn + 1 < nb ? dw.info(bn + 1) : infA;
+        }
+        dw.list(b, A, B, (unsigned)lane, loc, sx0, ys, valid);
     };
+    auto row_stage = [&](unsigned loc, int sx0, int ys, bool valid, D8Rows<BPP>& R) { io.rows(loc, sx0, ys, valid, R); };
+    auto convert = [&](const D8Rows<BPP>& R, double (&d)[64]) { io.convert(R, d); };
 
     // rows one batch ahead (kPF), or loaded at their batch -- grey windows
     // without the 24 prefetch registers fit three waves per SIMD, which the
@@ -1447,6 +1496,56 @@ __device__ __forceinline__ void fix_dense8_flat(const TileFixParams& tp, const d
         }
         if (v)
             p.out[(long long)(y - p.y0) * p.out_stride + x] =
+                edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
+    }
+}
+
+// The gather walk (N = 8): the small strips' entries pooled into full
+// 64-pixel batches of the flat list -- batch b's 64 entries lie in at most 64
+// consecutive slots from the batch map's first slot, so lane j loads slot
+// s0 + j and every lane finds the slot of its own entry by a binary search
+// over those offsets (shuffles), then refines its pixel like the dense walks.
+// Wave blk of nblk takes batches blk, blk + nblk, ...
+template <int BPP, int SEM>
+__device__ __forceinline__ void fix_gather8(const TileFixParams& tp, const double* lut, unsigned blk, unsigned nblk)
+{
+    const MapParams& p = tp.m;
+    const unsigned long long dc = *p.dense_ctr;
+    const unsigned nd = (unsigned)(dc >> 32), total = (unsigned)dc;
+    const unsigned spt = (unsigned)tp.tile_w / 64u, per_strip = 64u * (unsigned)p.tile_h;
+    const unsigned nstrips = (unsigned)tp.tiles_x * spt * (unsigned)((p.y1 - p.y0 + p.tile_h - 1) / p.tile_h);
+    if (nd > nstrips || total > nstrips * per_strip) return;   // uniform
+    const unsigned nb = (total + 63u) / 64u;
+    if (blk >= nb) return;                             // uniform
+    const unsigned lane = threadIdx.x;
+    const Win8Io<BPP, SEM> io(p, lut);
+    const unsigned* bslot = reinterpret_cast<const unsigned*>(p.dense_batch);
+    for (unsigned b = blk; b < nb; b += nblk) {        // uniform
+        const unsigned s0 = bslot[b];                  // slot of entry 64 b
+        const unsigned sj = s0 + lane;
+        uint2 v = make_uint2(0u, total);               // past the last slot: offset `total`
+        if (sj < nd) v = p.dense_list[sj];
+        const unsigned e = b * 64u + lane;
+        const bool valid = e < total;
+        // the last of the 64 slots whose first entry is at most e
+        int lo = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1)
+            if ((unsigned)__shfl((int)v.y, lo + step) <= e) lo += step;
+        const unsigned strip = (unsigned)__shfl((int)v.x, lo), off = (unsigned)__shfl((int)v.y, lo);
+        const unsigned loc = p.fix_list[valid ? strip * per_strip + (e - off) : 0u];
+        const unsigned tile = strip / spt;
+        const int sx0 = (int)(tile % (unsigned)tp.tiles_x) * tp.tile_w + 64 * (int)(strip % spt);
+        const int ys = p.y0 + (int)(tile / (unsigned)tp.tiles_x) * p.tile_h;
+        D8Rows<BPP> R;
+        io.rows(loc, sx0, ys, valid, R);
+        double d[64];
+        io.convert(R, d);
+        double m;
+        bool edge;
+        refine_regs<8>(d, tp.ct, m, edge);
+        if (valid)
+            p.out[(long long)(R.y - p.y0) * p.out_stride + R.x] =
                 edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
     }
 }
@@ -1727,10 +1826,11 @@ __global__ __launch_bounds__(64, DCTE_DENSE8_MINW) void dcte_fix_dense8(const Ti
 {
     constexpr bool kTab = SEM == kSemLqr && BPP == 3;
     __shared__ double lut[kTab ? 3 * 256 : 256];
-    if (!DCTE_FIX_FLAT && blockIdx.x >= *tp.m.dirty_count) return;   // uniform
+    if (!DCTE_FIX_FLAT && !kGather<8, SEM> && blockIdx.x >= *tp.m.dirty_count) return;   // uniform
     fill_luma_lut<kTab>(lut, threadIdx.x);
     wave_sync_lds();
-    fix_dense8<BPP, SEM>(tp, lut, blockIdx.x, gridDim.x);
+    if (DCTE_FIX_FLAT || blockIdx.x < *tp.m.dirty_count) fix_dense8<BPP, SEM>(tp, lut, blockIdx.x, gridDim.x);
+    if constexpr (kGather<8, SEM>) fix_gather8<BPP, SEM>(tp, lut, blockIdx.x, gridDim.x);
 }
 
 template <int N, int BPP, int SEM>
@@ -1791,10 +1891,11 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
             const unsigned blk = blockIdx.x - (unsigned)tp.sparse_blocks;
             const unsigned nblk = gridDim.x - (unsigned)tp.sparse_blocks;
             if constexpr (N == 8) {
-                if (!DCTE_FIX_FLAT && blk >= ndirty) return;   // uniform
+                if (!DCTE_FIX_FLAT && !kGather<N, SEM> && blk >= ndirty) return;   // uniform
                 fill_luma_lut<kTab>(lut, threadIdx.x);
                 wave_sync_lds();
-                fix_dense8<BPP, SEM>(tp, lut, blk, nblk);
+                if (DCTE_FIX_FLAT || blk < ndirty) fix_dense8<BPP, SEM>(tp, lut, blk, nblk);
+                if constexpr (kGather<N, SEM>) fix_gather8<BPP, SEM>(tp, lut, blk, nblk);
             } else {
                 fill_luma_lut<kTab16>(lut, threadIdx.x);
                 wave_sync_lds();
@@ -1893,7 +1994,7 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
             my_cnt = p.tile_count[my_strip];
         }
         if (tp.fix_total && sl == 0 && my_cnt) atomicAdd(tp.fix_total, my_cnt);
-        const bool sparse = my_cnt <= kFixDirect<N>;
+        const bool sparse = my_cnt <= kSparseMax<N, SEM>;
         const StripGeo sg = geo(my_strip);
         const unsigned smax = wave_max_u(sparse ? my_cnt : 0u);
         if constexpr (!kGroup) {
@@ -2438,9 +2539,10 @@ static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
         if (dev >= 0 && dev < kMaxDevices) cache[dev].store(resident, std::memory_order_relaxed);
     }
     const int blocks = nstrips < resident ? nstrips : resident;
-    if constexpr (kDenseFlat<N, SEM>) {
-        // the flat list's batch map first (one wave per possible dense strip)
-        hipLaunchKernelGGL((dcte_dense_index<kDenseBatch<N>>), dim3((nstrips + 3) / 4), dim3(256), 0, s, p);
+    if constexpr (kFlatList<N, SEM>) {
+        // the flat list's batch map first (one wave per possible listed strip)
+        hipLaunchKernelGGL((dcte_dense_index<kDenseBatch<N>, kGather<N, SEM>>), dim3((nstrips + 3) / 4), dim3(256), 0, s,
+                           p);
         if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
     }
     if constexpr (kDenseOwn<N, SEM>) {
@@ -2465,7 +2567,7 @@ static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
         }
         // flat list: up to one wave per batch the lists could hold; per-strip
         // walk (N = 8, DCTE_FIX_FLAT=0): one per strip
-        const long long most = kDenseFlat<N, SEM>
+        const long long most = kFlatList<N, SEM>
                                    ? ((long long)nstrips * 64 * p.m.tile_h + kDenseBatch<N> - 1) / kDenseBatch<N>
                                    : nstrips;
         const int dblocks = most < dres ? (int)most : dres;
@@ -2513,7 +2615,7 @@ hipError_t launch_fix_tiles(int n, int bpp, int sem, const TileFixParams& p, hip
 
 int dense_batch_entries(int n, int sem)
 {
-    if (n == 8) return kDenseFlat<8, kSemLqr> ? (int)kDenseBatch<8> : 0;
+    if (n == 8) return kFlatList<8, kSemLqr> ? (int)kDenseBatch<8> : 0;
     if (n == 16 && sem == kSemLqr) return kDenseFlat<16, kSemLqr> ? (int)kDenseBatch<16> : 0;
     return 0;
 }
