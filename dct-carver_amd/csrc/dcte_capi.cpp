@@ -27,9 +27,6 @@ namespace {
 constexpr double kDefaultTieTau = 4e-6;
 constexpr int kMaxGridY = 65535;   // launch grid limit in y (map tiles of a band)
 constexpr int kCountWords = 8;     // FixScratch::d_count
-#ifndef DCTE_WIDE_BANDS
-#define DCTE_WIDE_BANDS 1          // DCTE_OPT_WIDE_BANDS available (off by default)
-#endif
 
 struct FixScratch {
     // [0] list length (points / seam), [1] refined, [2 + phase] dirty strips of
@@ -120,7 +117,6 @@ struct dcte_ctx {
     bool dp_bandwise = false;       // DCTE_OPT_DP_BANDWISE
     unsigned dp_spin_limit = 0;     // DCTE_OPT_DP_SPIN_LIMIT (0: the kernel's default)
     unsigned long long* stamps = nullptr;   // DCTE_OPT_TSTAMP_BUF (timing-probe builds)
-    bool wide_bands = false;        // DCTE_OPT_WIDE_BANDS (A/B: lockstep tiles 10 % slower per band)
     std::vector<ProfEvent> prof;
     long long last_refined = 0;
     std::string last_error;
@@ -288,34 +284,27 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
 
     DCTE_HIP(ctx, hipSetDevice(d.id));
     // N = 8 launches of at most two rounds of workgroups (a strong-scaling
-    // rank's 2048- or 4096-row band): ordinary tiles whose waves step their
-    // priority down through the tile so the workgroups sharing a CU finish
-    // together (dcte_map's set_prio: 2048-row band -6 %, 4096 rows -2.5 %,
-    // profiles/r02/map_fair_ab.jsonl), or, on request (DCTE_OPT_WIDE_BANDS),
-    // 1024-thread workgroups whose waves move through their tile in lockstep
-    // (Geo WIDE in dcte_kernels.hip): every CU then stays busy to the end
-    // (97 % slot-busy vs 87 %) but the lockstep tile runs 20 % slower, so the
-    // band takes 0.193 vs 0.176 ms (profiles/r03/band_wide_ab.jsonl); longer
-    // launches even out by themselves
+    // rank's 2048- or 4096-row band): the waves step their priority down
+    // through the tile so the workgroups sharing a CU finish together
+    // (dcte_map's set_prio: 2048-row band -6 %, 4096 rows -2.5 %,
+    // profiles/r02/map_fair_ab.jsonl); longer launches even out by themselves.
+    // (1024-thread lockstep tiles kept every CU busy to the end, 97 % slot-busy
+    // vs 87 %, but ran each tile 20 % slower: profiles/r03/band_wide_ab.jsonl.)
     int fair = 0;
-    bool wide = false;
     if (n == 8) {
         if (d.cus <= 0 &&
             hipDeviceGetAttribute(&d.cus, hipDeviceAttributeMultiprocessorCount, d.id) != hipSuccess)
             d.cus = 256;
         const long long nwg = (long long)dcte::map_tiles_x(n, w) * dcte::map_tiles_y(n, y1 - y0, tile_h);
-        if (nwg <= 2LL * 4 * d.cus) {
-            if (DCTE_WIDE_BANDS && ctx->wide_bands) wide = true;
-            else fair = 3;
-        }
+        if (nwg <= 2LL * 4 * d.cus) fair = 3;
     }
     // refinement lists: one region of 64 * tile_h entries per 64-column strip
-    const int tiles_x = dcte::map_tiles_x(n, w, wide), tiles_y = dcte::map_tiles_y(n, y1 - y0, tile_h);
+    const int tiles_x = dcte::map_tiles_x(n, w), tiles_y = dcte::map_tiles_y(n, y1 - y0, tile_h);
     if (tiles_y > kMaxGridY) {
         ctx->last_error = "tile rows exceed the launch grid (raise DCTE_OPT_TILE_H)";
         return DCTE_ERANGE;
     }
-    const size_t ntiles = (size_t)tiles_x * (size_t)tiles_y * (size_t)dcte::map_strips_per_tile(n, wide);
+    const size_t ntiles = (size_t)tiles_x * (size_t)tiles_y * (size_t)dcte::map_strips_per_tile(n);
     const size_t list_len = ntiles * 64 * (size_t)tile_h;
     if (list_len >= (1ULL << 32)) return DCTE_ERANGE;
     FixScratch* f = nullptr;
@@ -323,8 +312,8 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     if (rc) return rc;
     rc = ensure_tiles(ctx, f, ntiles);
     if (rc) return rc;
-    // the dense refinement's batch map (N = 16 liblqr; N = 8 in flat-walk
-    // builds): one uint4 per batch the lists can hold
+    // the dense refinement's batch map (N = 16 liblqr): one uint4 per batch
+    // the lists can hold
     if (const int epb = dcte::dense_batch_entries(n, sem)) {
         rc = ensure_buf(ctx, &f->d_batch, &f->bcap, (list_len / (size_t)epb + 1) * 16);
         if (rc) return rc;
@@ -342,7 +331,6 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     p.y1 = y1;
     p.tile_h = tile_h;
     p.fair = fair;
-    p.wide = wide ? 1 : 0;
     p.out = d_out;
     p.out_stride = out_stride;
     p.we = (float)((double)edges / scale);
@@ -366,7 +354,7 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     small_twiddles(n, q.ct);
     q.fix_total = f->d_count + 1;
     q.tiles_x = tiles_x;
-    q.tile_w = dcte::map_tile_w(n, wide);
+    q.tile_w = dcte::map_tile_w(n);
 
     // Any failure from here on leaves both dirty counters zeroed on the
     // stream: a map launch that never ran did not zero its successor's counter,
@@ -685,9 +673,6 @@ int dcte_set_option(dcte_ctx* ctx, int option, double value)
         // band-wise launches
         for (Device& d : ctx->devs)
             for (auto& kv : d.dp) kv.second.max_tiles = -1;
-        return DCTE_OK;
-    case DCTE_OPT_WIDE_BANDS:
-        ctx->wide_bands = value != 0;
         return DCTE_OK;
     case DCTE_OPT_TSTAMP_BUF:
         // a device address (exact in a double below 2^53); 0 = none
@@ -1159,7 +1144,7 @@ int dcte_carver_create(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, 
     c->bpp = bpp;
     c->n = n;
     c->r = n / 2;                    // the radius the plug-in registers (src/render.c:314-315)
-    c->bw = 4 * c->r + 4;
+    c->bw = 8 * c->r + 4;            // reading windows of the update band too (dcte_band_gather)
     c->edges = edges;
     c->textures = textures;
     c->pitch = (size_t)c->W0 * bpp;

@@ -21,7 +21,6 @@ struct MapParams {
     int y0, y1;              // output rows (global)
     int tile_h;              // output rows per workgroup
     int fair;                // > 0: priority levels a workgroup steps down through its tile
-    int wide;                // N = 8: 1024-column tiles of 1024-thread workgroups (Geo WIDE)
     float* out;              // row y at out + (y - y0) * out_stride
     long long out_stride;    // floats
     float we, wt;            // edges / textures weights, pre-scaled to luma units
@@ -48,8 +47,8 @@ struct MapParams {
     unsigned long long* dense_next;
     uint2* dense_list;
     // and (written by dcte_dense_index, between the map launch and its
-    // refinement) per refinement batch b (kDenseBatch entries of the flat list,
-    // 64 at N = 8, 16 at N = 16) the dense strip holding its first entry:
+    // refinement) per refinement batch b (16 entries of the flat list, N = 16
+    // liblqr) the dense strip holding its first entry:
     // {its first column, its tile's first output row, strip, offset of its
     // first entry in the flat list}
     uint4* dense_batch;
@@ -166,11 +165,11 @@ int dp_super_bands();
 int dp_max_tiles(int device);
 
 // geometry the launcher uses (exported for tests / bench)
-int map_tile_w(int n, bool wide = false);
+int map_tile_w(int n);
 int map_default_tile_h(int n);
-int map_tiles_x(int n, int w, bool wide = false);   // map grid (tiles) of a launch
+int map_tiles_x(int n, int w);   // map grid (tiles) of a launch
 int map_tiles_y(int n, int rows, int tile_h);
-int map_strips_per_tile(int n, bool wide = false);
+int map_strips_per_tile(int n);
 int dense_batch_entries(int n, int sem);   // entries per dense refinement batch (0: no flat list)
 
 }  // namespace dcte

@@ -39,116 +39,55 @@
 
 namespace dcte {
 
-// build-time tuning knobs (tools/variants.sh A/Bs them on the GPU)
+// Build-time tuning values.  Each can be overridden with -D (tools/variants.sh
+// builds such variants for A/Bs on the GPU; tests/test_knob_builds.py compiles
+// every one of them with a non-default value).  The losing code paths of
+// earlier A/Bs are gone from the source; their records stay in profiles/.
 #ifndef DCTE_WG8
-#define DCTE_WG8 256       // threads per workgroup (= strip width) at N = 8 (64: +0.3 % with DCTE_SC, 4x the halo reads)
+#define DCTE_WG8 256       // threads per workgroup (= strip width) at N = 8 (64: +0.3 %, 4x the halo reads)
 #endif
 #ifndef DCTE_TILE_H
-#define DCTE_TILE_H 128
+#define DCTE_TILE_H 128    // output rows per map workgroup, N <= 8
 #endif
 #ifndef DCTE_TILE_H16
-#define DCTE_TILE_H16 128
+#define DCTE_TILE_H16 128  // ... N = 16
 #endif
 #ifndef DCTE_G8
 #define DCTE_G8 8          // rows per staging group for N = 8 (multiple of 8)
 #endif
 #ifndef DCTE_MIN_WAVES
-#define DCTE_MIN_WAVES 4   // __launch_bounds__ minimum waves per SIMD (<= 128 VGPRs; N = 16 would take 134)
-#endif
-#ifndef DCTE_DB
-#define DCTE_DB 1          // N <= 8: double-buffered LDS staging, one barrier per row group
+#define DCTE_MIN_WAVES 4   // __launch_bounds__ minimum waves per SIMD (<= 128 VGPRs)
 #endif
 #ifndef DCTE_MIN_WAVES16
-#define DCTE_MIN_WAVES16 4 // the same for N = 16
-#endif
-#ifndef DCTE_XCD
-#define DCTE_XCD 1         // XCD-contiguous tile order (neighbouring strips share an L2)
-#endif
-#ifndef DCTE_PRIO
-#define DCTE_PRIO 1        // wave priority while staging / converting a group (A/B: -2 % at N = 8 and 16)
+#define DCTE_MIN_WAVES16 4 // the same for N = 16 (it would take 134 VGPRs and 3 waves: -2 % with the cap)
 #endif
 #ifndef DCTE_TSTAMP
-#define DCTE_TSTAMP 0      // timing-probe builds: per-workgroup timestamps over the output (tools/tstamp.py)
+#define DCTE_TSTAMP 0      // timing-probe builds: per-workgroup timestamps (tools/tstamp.py)
 #endif
 #ifndef DCTE_PF2_MAXN
 #define DCTE_PF2_MAXN 4    // N <= this: raw rows prefetched two groups ahead (else one)
 #endif
-#ifndef DCTE_XBAL
-#define DCTE_XBAL 1        // halo-column luma conversions spread one per lane of the last wave
-#endif
-#ifndef DCTE_CONV_BAL
-#define DCTE_CONV_BAL 0    // N = 16: luma conversions spread over all threads of the workgroup
-#endif
-#ifndef DCTE_EMIT_NB
-#define DCTE_EMIT_NB 1     // store without a branch on the column (out-of-frame lanes dropped by the bounds check)
-#endif
-#ifndef DCTE_DIRECT
-#define DCTE_DIRECT 1      // N = 8: each lane loads its own pixel's bytes (dwordx2), no raw LDS stage (-1.8 %)
-#endif
-#ifndef DCTE_DOT4
-#define DCTE_DOT4 1        // liblqr RGB luma through two v_dot4_u32_u8 (4 ops instead of ~8)
-#endif
+constexpr int kPrio = 1;   // wave priority while staging / converting a group (A/B: -2 % at N = 8 and 16)
 constexpr unsigned kBufFlags = 0x00020000u;  // gfx9 raw buffer dword3
 
 // refinement (below): strips with at most kFixDirect<N> flagged pixels are
 // "sparse" (dcte_fix_strips gathers their windows directly), the rest dense
-#ifndef DCTE_FIX_LANES
-#define DCTE_FIX_LANES 1 // dense strips at N = 8: one lane per pixel, window in registers
-#endif
-#ifndef DCTE_FIX_FLAT
-// ... taken from one flat list of all dense entries, 64 at a time, pipelined
-// (fix_dense8_flat).  Off: one wave walks whole strips (fix_dense8_run),
-// which keeps the window rows of a strip in the wave's L1 and the grey walk
-// at 162 VGPRs (3 waves per SIMD).  A/B at 16384^2 (profiles/r03/dense_flat_ab.jsonl):
-// the flat walk wins where dense strips are short (dots -20 %, text -25 %)
-// and loses where they are long (line art +8 %, the 8-px grid +16..22 %)
-#define DCTE_FIX_FLAT 0
-#endif
 #ifndef DCTE_FIX_DIRECT8
-#define DCTE_FIX_DIRECT8 16u    // N <= 8: most flagged pixels a strip may hold and still be sparse (128 before: dots +47 %, text +4 %; profiles/r03/fix_direct_ab.jsonl)
+#define DCTE_FIX_DIRECT8 16u    // N = 8: most flagged pixels a strip may hold and still be sparse (128 before: dots +47 %, text +4 %; profiles/r03/fix_direct_ab.jsonl)
 #endif
 template <int N>
 constexpr unsigned kFixDirect = N == 16 ? 32u : (unsigned)DCTE_FIX_DIRECT8;
-#ifndef DCTE_FIX_QUAD16
-#define DCTE_FIX_QUAD16 1 // dense strips at N = 16 (liblqr): four lanes per pixel, window in registers
-#endif
-// dense strips walked by a lane-per-pixel / lane-quad-per-pixel kernel of
-// their own (fix_dense8*, fix_dense16_flat) rather than the band path of
-// dcte_fix_strips
+// dense strips walked by a lane-per-pixel (N = 8, fix_dense8_run) /
+// lane-quad-per-pixel (N = 16 liblqr, fix_dense16_flat) walk rather than the
+// band path of dcte_fix_strips
 template <int N, int SEM>
-constexpr bool kDenseOwn = (N == 8 && DCTE_FIX_LANES) || (N == 16 && SEM == kSemLqr && DCTE_FIX_QUAD16);
-// ... from the flat list the map kernel numbers (MapParams::dense_list)
+constexpr bool kDenseOwn = N == 8 || (N == 16 && SEM == kSemLqr);
+// ... N = 16 from the flat list the map kernel numbers (MapParams::dense_list)
 template <int N, int SEM>
-constexpr bool kDenseFlat = (N == 8 && DCTE_FIX_LANES && DCTE_FIX_FLAT) || (N == 16 && kDenseOwn<N, SEM>);
-// entries per refinement batch of the flat list: a lane per pixel at N = 8,
-// a quad of lanes at N = 16
-template <int N>
-constexpr unsigned kDenseBatch = N == 8 ? 64u : 16u;
-#ifndef DCTE_FIX_GATHER
-#define DCTE_FIX_GATHER 0       // N = 8: strips of at most DCTE_GATHER_MAX flags pooled into full 64-pixel batches (measured slower: profiles/r03/gather_ab.jsonl)
-#endif
-#ifndef DCTE_GATHER_MAX
-#define DCTE_GATHER_MAX 128u
-#endif
-// N = 8 with the gather walk (fix_gather8): the flat list holds the SMALL
-// strips (1 .. kGatherMax flags), pooled 64 pixels per batch whatever their
-// strips; longer strips keep the per-strip walk and nothing is left sparse
-template <int N, int SEM>
-constexpr bool kGather = N == 8 && DCTE_FIX_LANES && !DCTE_FIX_FLAT && DCTE_FIX_GATHER;
-constexpr unsigned kGatherMax = DCTE_GATHER_MAX;
-// the map kernel fills the flat list (dense strips, or gathered small ones)
-template <int N, int SEM>
-constexpr bool kFlatList = kDenseFlat<N, SEM> || kGather<N, SEM>;
-// most flags a strip may hold and still go to dcte_fix_strips' sparse walk
-template <int N, int SEM>
-constexpr unsigned kSparseMax = kGather<N, SEM> ? 0u : kFixDirect<N>;
-// fewest flags (exclusive) of a strip the per-strip dense walk takes
-template <int N, int SEM>
-constexpr unsigned kDenseMin = kGather<N, SEM> ? kGatherMax : kFixDirect<N>;
-// the flat walk's batches span at most two strips only if a dense strip
-// holds more entries than a batch
-static_assert(!kDenseFlat<8, kSemLqr> || kFixDirect<8> >= kDenseBatch<8>, "DCTE_FIX_FLAT needs DCTE_FIX_DIRECT8 >= 64");
-static_assert(!kDenseFlat<16, kSemLqr> || kFixDirect<16> >= kDenseBatch<16>, "N = 16 dense batches");
+constexpr bool kDenseFlat = N == 16 && kDenseOwn<N, SEM>;
+// entries per refinement batch of the flat list (a quad of lanes per pixel)
+constexpr unsigned kDenseBatch16 = 16u;
+static_assert(kFixDirect<16> >= kDenseBatch16, "N = 16 dense batches");
 
 // SEM = kSemLqr    : liblqr callback window, offsets -(N/2-1)..N/2
 //                    (src/render.c:146-152), liblqr luma (dcte_luma.h)
@@ -163,17 +102,9 @@ struct MapThreads {
     static constexpr int min_waves = N == 16 ? DCTE_MIN_WAVES16 : DCTE_MIN_WAVES;
 };
 
-// WIDE (N = 8 only): one 1024-thread workgroup per tile of 1024 columns, so
-// a CU holds one workgroup whose sixteen waves move through the tile in
-// lockstep (one barrier per row group) -- used for launches of at most two
-// rounds of ordinary tiles (a strong-scaling rank's band), where the four
-// independent workgroups of a CU otherwise finish far apart (the SIMDs issue
-// the oldest wave first) and the launch's tail runs below occupancy.
-constexpr int kWideThreads = 1024;
-
-template <int N, int SEM, bool WIDE = false>
+template <int N, int SEM>
 struct Geo {
-    static constexpr int T = WIDE ? kWideThreads : MapThreads<N>::value;   // threads per workgroup
+    static constexpr int T = MapThreads<N>::value;       // threads per workgroup
     static constexpr int S = Lanes<N>::S;                // lanes per output column
     static constexpr int CH = Lanes<N>::CH;              // k1 channels per lane
     static constexpr int TW = T / S;              // output columns per WG
@@ -202,10 +133,10 @@ __device__ __forceinline__ void static_for(F&& f)
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 // ------------------------------------------------------------------ main kernel
-template <int N, int BPP, int SEM, bool WIDE>
-__global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) void dcte_map(const MapParams p)
+template <int N, int BPP, int SEM>
+__global__ __launch_bounds__((Geo<N, SEM>::T), MapThreads<N>::min_waves) void dcte_map(const MapParams p)
 {
-    using Gm = Geo<N, SEM, WIDE>;
+    using Gm = Geo<N, SEM>;
     constexpr int kThreads = Gm::T;
     constexpr int S = Gm::S, CH = Gm::CH, TW = Gm::TW, HL = Gm::HL;
     constexpr int LW = Gm::LW, LWP = Gm::LWP, G = Gm::G;
@@ -214,10 +145,10 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
 
     // N <= 8: raw / lum double-buffered, so a row group needs one barrier
     // (N = 16 keeps one buffer: its LDS combine of partial maxima adds one anyway)
-    constexpr bool kDB = DCTE_DB && S == 1;
+    constexpr bool kDB = S == 1;
     constexpr int NB = kDB ? 2 : 1;
-    // DCTE_DIRECT (below) needs no raw stage
-    constexpr bool kDirectLds = DCTE_DIRECT && S == 1 && kDB && !(N <= DCTE_PF2_MAXN) &&
+    // the direct loads (below) need no raw stage
+    constexpr bool kDirectLds = S == 1 && kDB && !(N <= DCTE_PF2_MAXN) &&
                                 LW - kThreads > 0 && (LW - kThreads) * G <= 64;
     __shared__ uint32_t raw[kDirectLds ? 1 : NB][kDirectLds ? 1 : G][kDirectLds ? 1 : NDW];
     __shared__ float lum[NB][G][LWP];
@@ -240,7 +171,7 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
     int bx = blockIdx.x, by = blockIdx.y;
-    if constexpr (DCTE_XCD) {
+    {
         const int nwg = gridDim.x * gridDim.y, L = blockIdx.x + gridDim.x * blockIdx.y;
         const int q = nwg / 8, r = nwg % 8, xcd = L % 8;
         const int T = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / 8;
@@ -286,7 +217,7 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
 
     // raw rows in flight: PFD groups ahead (two register buffers for the
     // small blocks, whose launches are bound by loads in flight, not VALU)
-    constexpr int PFD = (S == 1 && DCTE_DB && N <= DCTE_PF2_MAXN) ? 2 : 1;
+    constexpr int PFD = (S == 1 && N <= DCTE_PF2_MAXN) ? 2 : 1;
     uint32_t pref[PFD][G][DPT];
     auto issue = [&](int g, auto PB) {
 #pragma unroll
@@ -301,14 +232,15 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
         }
     };
 
-    // DCTE_DIRECT: no raw stage in LDS.  Each lane fetches the bytes of its
-    // own column of each row of a group with one 8-byte buffer load (any
-    // alignment: the pixel's <= 4 bytes lie inside it), one group ahead, and
-    // converts them straight from registers; the last wave's lanes also fetch
-    // the N - 1 halo columns' pixels (one (row, column) each, as DCTE_XBAL).
+    // Direct loads (N = 8): no raw stage in LDS.  Each lane fetches the bytes
+    // of its own column of each row of a group with one 8-byte buffer load
+    // (any alignment: the pixel's <= 4 bytes lie inside it), one group ahead,
+    // and converts them straight from registers; the last wave's lanes also
+    // fetch the N - 1 halo columns' pixels (one (row, column) each, as in
+    // convert()).
     // The convert phase then waits on no LDS reads.
     constexpr int XH = LW - kThreads;                  // halo columns past one per lane
-    constexpr bool kDirect = DCTE_DIRECT && S == 1 && kDB && PFD == 1 && XH > 0 && XH * G <= 64;
+    constexpr bool kDirect = S == 1 && kDB && PFD == 1 && XH > 0 && XH * G <= 64;
     static_assert(kDirect == kDirectLds, "raw stage sizing");
     uint32_t dlo[kDirect ? G : 1], dhi[kDirect ? G : 1];
     uint32_t xlo = 0, xhi = 0;
@@ -347,7 +279,7 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
     auto luma_bytes = [&](uint32_t wd) -> float {       // exact integer luma (biased) of a pixel's bytes
         const uint32_t c0 = wd & 255u, c1 = BPP >= 3 ? (wd >> 8) & 255u : 0u, c2 = BPP >= 3 ? (wd >> 16) & 255u : 0u;
         int L;
-        if constexpr (SEM == kSemLqr && BPP >= 3 && DCTE_DOT4) {
+        if constexpr (SEM == kSemLqr && BPP >= 3) {
             // L = 1063 R + 3576 G + 361 B - 637500 with the byte dot products:
             // the weights split into 256 hi + lo (4 / 39, 13 / 248, 1 / 105),
             // the bias in the lo sum's accumulator (mod 2^32); the fourth byte
@@ -383,8 +315,6 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
     };
 
     float ring[N][CH];
-    // matrix-pipe operands of the N = 8 texture columns (every lane active here)
-    const Mfma8K mk8 = (N == 8 && DCTE_MFMA8 > 0) ? mfma8_consts() : Mfma8K{};
     const float we = p.we, wt = p.wt;
     // output rows [ys, ye) of this workgroup through one buffer resource
     const int ostride4 = (int)(p.out_stride * 4);
@@ -411,17 +341,11 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
 
     // decision + store (+ refinement flag) of output pixel (x, y)
     auto emit = [&](int y, int xx, float mt, float me) {
-#if DCTE_EMIT_NB
         // no branch on the column: a lane past the frame's last column stores
         // at the resource's size, which the bounds check drops (the wave's
         // row offset rides in soffset, so the sum stays below 2^32)
         const bool inside = xx < w;
         const uint32_t voff = inside ? (uint32_t)xx * 4u : orec;
-#else
-        if (xx >= w) return;
-        const bool inside = true;
-        const uint32_t voff = (uint32_t)xx * 4u;
-#endif
         const bool edge = me > mt;
         // the product, then the select (the weights stay in SGPRs)
         const float e_out = me * we, t_out = mt * wt;
@@ -479,7 +403,7 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
     };
     auto convert = [&](int gg, int b) {
         constexpr int X = LW - kThreads;                 // halo columns past one per lane
-        if constexpr (DCTE_XBAL && X > 0 && X * G <= 64) {
+        if constexpr (X > 0 && X * G <= 64) {
             // one column per lane for all G rows; the X * G halo conversions
             // go one per lane to the last wave instead of G rows to X lanes
             // of the first (which would hold the whole workgroup at the barrier)
@@ -487,11 +411,6 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
             for (int u = 0; u < G; u++) luma_at(gg, b, u, tx);
             const int l = tx - (kThreads - 64);
             if (l >= 0 && l < X * G) luma_at(gg, b, l / X, kThreads + l % X);
-        } else if constexpr (DCTE_CONV_BAL && LW < kThreads) {
-            // fewer columns than threads (N = 16: 79 of 256): the LW x G
-            // conversions spread over every thread, not G rows on LW threads
-            // (which held two waves busy while two idled before the barrier)
-            for (int e = tx; e < LW * G; e += kThreads) luma_at(gg, b, e / LW, e % LW);
         } else {
             for (int cc = tx; cc < LW; cc += kThreads) {
 #pragma unroll
@@ -518,10 +437,7 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
                 }
                 if (i >= N - 1) {
                     float mt, me;
-                    if constexpr (N == 8 && DCTE_MFMA8 > 0)
-                        Cols<N>::template run<(u + 1) % N, true>(ring, lane_p, mt, me, mk8);
-                    else
-                        Cols<N>::template run<(u + 1) % N>(ring, lane_p, mt, me);
+                    Cols<N>::template run<(u + 1) % N>(ring, lane_p, mt, me);
                     if constexpr (S == 4) {
                         part_t[u][lane_p][c] = mt;
                         if ((lane_p & 1) == 0) part_e[u][lane_p >> 1][c] = me;
@@ -548,7 +464,7 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
     };
 
     // Wave priority.  A wave stages and converts a group at a raised
-    // priority so its workgroup reaches the barrier sooner (DCTE_PRIO).  In
+    // priority so its workgroup reaches the barrier sooner (kPrio).  In
     // launches of one or two rounds (p.fair > 0, set by the host) the level
     // also falls as the workgroup gets through its tile: the hardware
     // otherwise favours the OLDEST waves of a SIMD, so of the workgroups
@@ -556,9 +472,9 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
     // the CU runs the launch's tail below occupancy (tools/tstamp.py, one
     // round of 128-row tiles: 115-202 us for identical tiles, 137-185 with
     // the falling level).
-    const int fair = (N == 8 && !WIDE) ? p.fair : 0; // uniform; the host sets it for N = 8 only
+    const int fair = N == 8 ? p.fair : 0;            // uniform; the host sets it for N = 8 only
     auto set_prio = [&](bool staging, int g) __attribute__((always_inline)) {
-        int lvl = staging ? DCTE_PRIO : 0;
+        int lvl = staging ? kPrio : 0;
         if (fair > 0) lvl += (fair - 1) - min(fair - 1, g * fair / ngroups);
         if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
         else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
@@ -578,18 +494,14 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
         if (ngroups > 2) issue(2, P0);
         __syncthreads();
         auto step = [&](int g, int b, auto PB) __attribute__((always_inline)) {
-#if DCTE_PRIO
             set_prio(true, g);
-#endif
             convert(g, b);
             if (g + 1 < ngroups) {
                 stage(g + 1, b ^ 1, PB);
                 if (g + 3 < ngroups) issue(g + 3, PB);
             }
             __syncthreads();
-#if DCTE_PRIO
             set_prio(false, g);
-#endif
             compute(g, b);
         };
         for (int g = 0; g < ngroups; g += 2) {
@@ -604,15 +516,11 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
         issue_direct(0);
         for (int g = 0; g < ngroups; g++) {
             const int b = g & 1;
-#if DCTE_PRIO
             set_prio(true, g);
-#endif
             convert_direct(g, b);
             if (g + 1 < ngroups) issue_direct(g + 1);
             __syncthreads();
-#if DCTE_PRIO
             set_prio(false, g);
-#endif
             compute(g, b);
         }
     } else if constexpr (kDB) {
@@ -625,34 +533,26 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
         __syncthreads();
         for (int g = 0; g < ngroups; g++) {
             const int b = g & 1;
-#if DCTE_PRIO
             set_prio(true, g);
-#endif
             convert(g, b);
             if (g + 1 < ngroups) {
                 stage(g + 1, b ^ 1, P0);
                 if (g + 2 < ngroups) issue(g + 2, P0);
             }
             __syncthreads();
-#if DCTE_PRIO
             set_prio(false, g);
-#endif
             compute(g, b);
         }
     } else {
         for (int g = 0; g < ngroups; g++) {
             // stage raw bytes of group g, then prefetch group g + 1
-#if DCTE_PRIO
             set_prio(true, g);
-#endif
             stage(g, 0, P0);
             if (g + 1 < ngroups) issue(g + 1, P0);
             __syncthreads();
             convert(g, 0);
             __syncthreads();
-#if DCTE_PRIO
             set_prio(false, g);
-#endif
             compute(g, 0);
         }
     }
@@ -663,7 +563,7 @@ __global__ __launch_bounds__((Geo<N, SEM, WIDE>::T), MapThreads<N>::min_waves) v
             const unsigned st = strip - sc + tx;
             p.tile_count[st] = cnt;
             p.dirty_list[atomicAdd(p.dirty_count, 1u)] = st;
-            if ((kDenseFlat<N, SEM> && cnt > kFixDirect<N>) || (kGather<N, SEM> && cnt <= kGatherMax)) {
+            if (kDenseFlat<N, SEM> && cnt > kFixDirect<N>) {
                 const unsigned long long r = atomicAdd(p.dense_ctr, (1ull << 32) | cnt);
                 const unsigned slot = (unsigned)(r >> 32), off = (unsigned)r;
                 // a launch holds gridDim.x * gridDim.y * SPT strips (the guard only
@@ -790,19 +690,16 @@ __device__ __forceinline__ void lastmax_group(const double* v, int l, double& m,
 #ifndef DCTE_FIX_IL
 #define DCTE_FIX_IL 1    // N = 8 register path: 8-point steps the scheduler may interleave
 #endif
-// FIRST = false: the caller already ran the first pass (dcte_fix_dense8)
-template <int N, int IL = DCTE_FIX_IL, bool FIRST = true>
+template <int N, int IL = DCTE_FIX_IL>
 __device__ __forceinline__ void refine_regs(double (&d)[N * N], const double* ct, double& m, bool& edge)
 {
     if constexpr (N == 8) {
         // IL 8-point steps at a time: interleaving all eight would need their
         // temporaries live beside the 64-element window (> 256 registers)
-        if constexpr (FIRST) {
 #pragma unroll
-            for (int i = 0; i < 8; i++) {
-                r64::step8(d + i, 8);
-                if ((i + 1) % IL == 0) __builtin_amdgcn_sched_barrier(0);
-            }
+        for (int i = 0; i < 8; i++) {
+            r64::step8(d + i, 8);
+            if ((i + 1) % IL == 0) __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
         for (int i = 0; i < 8; i++) {
@@ -821,45 +718,6 @@ __device__ __forceinline__ void refine_regs(double (&d)[N * N], const double* ct
 #pragma unroll
     for (int e = N + 1; e < N * N; e++) ma = fmax(ma, fabs(d[e]));
     lastmax_decide(fabs(d[1]), fabs(d[N]), mb, ma, m, edge);
-}
-
-// N = 8, first pass done: the second pass and the last-maximum scan, with
-// columns that cannot hold the maximum skipped.  The second pass is
-// orthonormal (ddct8x8s, src/fft2d/shrtdct.c:90-117), so every output of
-// coefficient row k1 is at most the row's norm ||F[k1][.]|| (up to ~1e-15
-// relative rounding): once rows 0 and 1 (the two edge atoms) are transformed,
-// a row whose squared norm, with a 1e-12 relative margin, is below the square
-// of the running maximum can neither be the maximum nor tie it, and the
-// last-maximum scan (lastmax_decide) never looks at it.  The skip is taken
-// only when no lane of the wave needs the row (lane-per-pixel path).
-__device__ __forceinline__ void refine8_second_skip(double (&d)[64], double& m, bool& edge)
-{
-    r64::step8(d, 1);
-    r64::step8(d + 8, 1);
-    const double a01 = fabs(d[1]), a10 = fabs(d[8]);
-    double mb = -1.0, ma = -1.0;
-#pragma unroll
-    for (int e = 2; e < 8; e++) mb = fmax(mb, fabs(d[e]));
-#pragma unroll
-    for (int e = 9; e < 16; e++) ma = fmax(ma, fabs(d[e]));
-    double run = fmax(fmax(a01, a10), fmax(mb, ma));
-#pragma unroll
-    for (int k = 2; k < 8; k++) {
-        double n2 = 0.0;
-#pragma unroll
-        for (int j = 0; j < 8; j++) n2 = fma(d[8 * k + j], d[8 * k + j], n2);
-        const bool need = n2 * (1.0 + 1e-12) >= run * run * (1.0 - 1e-12);
-        if (__any(need)) {                            // uniform
-            r64::step8(d + 8 * k, 1);
-            double cm = -1.0;
-#pragma unroll
-            for (int j = 0; j < 8; j++) cm = fmax(cm, fabs(d[8 * k + j]));
-            ma = fmax(ma, cm);
-            run = fmax(run, cm);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    lastmax_decide(a01, a10, mb, ma, m, edge);
 }
 
 __device__ __forceinline__ void wave_sync_lds()
@@ -962,13 +820,6 @@ __global__ __launch_bounds__(kFixThreads) void dcte_fix(const FixParams p)
 // flagged at 16384^2: 0.17 ms vs 0.24 at 128, 0.16 at 8 where text loses
 // 10 %; profiles/r03/fix_direct_ab.jsonl -- with the band path of r02 the
 // best was 128), N = 16 at 32 (profiles/r02/fix_direct.jsonl).
-#ifndef DCTE_FIX_ALIGNED
-#define DCTE_FIX_ALIGNED 1  // dense strips read the staged raw bytes as aligned dwords
-#endif
-#ifndef DCTE_FIX_PIPE
-#define DCTE_FIX_PIPE 1  // sparse strips (N = 8, 16): dword row fetches, next window in flight
-#endif
-
 
 template <int N, int SEM>
 struct FixStrip {
@@ -1024,18 +875,15 @@ __device__ __forceinline__ void refine_group(const double* lum, int LW, int at, 
                       w, l, best, edge);
 }
 
-#ifndef DCTE_FIX_MERGE
-#define DCTE_FIX_MERGE 1 // ... run by extra blocks of the dcte_fix_strips launch (one launch less)
-#endif
-// grey layers at N <= 8 fit 128 VGPRs: 4 waves per SIMD (the LDS allows them)
+// grey layers at N <= 4 fit 128 VGPRs: 4 waves per SIMD (the LDS allows them)
 #ifndef DCTE_FIX_MINW
 #define DCTE_FIX_MINW 4
 #endif
 #ifndef DCTE_FIX_MINW_LANES
-#define DCTE_FIX_MINW_LANES 2   // N = 8 with lane-per-pixel dense strips: the window alone is 128 VGPRs
+#define DCTE_FIX_MINW_LANES 2   // N = 8 (lane-per-pixel dense strips in the same launch): the window alone is 128 VGPRs
 #endif
 template <int N, int BPP>
-constexpr int kFixMinWaves = (BPP == 1 && N <= 8) ? ((N == 8 && DCTE_FIX_LANES) ? DCTE_FIX_MINW_LANES : DCTE_FIX_MINW) : 1;
+constexpr int kFixMinWaves = (BPP == 1 && N <= 8) ? (N == 8 ? DCTE_FIX_MINW_LANES : DCTE_FIX_MINW) : 1;
 
 // Dense strips at N = 8 (more than kFixDirect<8> flagged pixels; the sparse
 // ones stay with dcte_fix_strips): one lane per flagged pixel, its whole
@@ -1046,30 +894,10 @@ constexpr int kFixMinWaves = (BPP == 1 && N <= 8) ? ((N == 8 && DCTE_FIX_LANES) 
 // step -- eight independent 8-point transforms per pass keep the lane busy
 // where the group-per-window form of dcte_fix_strips waited on LDS transposes
 // (line art RGB at 16384^2: 1.27 -> 0.46 ms, profiles/r03/fix_lanes_ab.jsonl).
-// A kernel of its own: no band staging, so only the tables take LDS and the
-// register count sets the occupancy.  Waves take dirty strips in turn.
-#ifndef DCTE_DENSE8_MINW
-#define DCTE_DENSE8_MINW 2
-#endif
-#ifndef DCTE_DENSE8_PF
-#define DCTE_DENSE8_PF 1        // flat walk: a batch's window rows load during the previous batch
-#endif
-#ifndef DCTE_DENSE8_PF_GREY
-#define DCTE_DENSE8_PF_GREY 0   // ... not for grey layers (162 VGPRs: 3 waves per SIMD)
-#endif
+// Extra blocks of the dcte_fix_strips launch: no band staging, so only the
+// tables take LDS.  Waves take dirty strips in turn.
 #ifndef DCTE_DENSE8_RB
 #define DCTE_DENSE8_RB 8      // window rows per load batch
-#endif
-#ifndef DCTE_DENSE8_FUSE
-#define DCTE_DENSE8_FUSE 0    // liblqr: first-pass step of each row as soon as it is converted
-#endif
-#ifndef DCTE_DENSE8_SKIP
-#define DCTE_DENSE8_SKIP 0    // skip second-pass rows whose norm is below the running maximum
-#endif
-// timing-probe builds only (wrong results): 1 = no table reads (luma = first
-// byte), 2 = no transform, 3 = no row loads
-#ifndef DCTE_DENSE8_PROBE
-#define DCTE_DENSE8_PROBE 0
 #endif
 // the 256 liblqr channel quotients v / 255 (pre-weighted per channel for
 // liblqr RGB: kTab), as the reference divides (bit-identical)
@@ -1110,7 +938,6 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
     // liblqr luma (src/render.c:315, LQR_ER_LUMA) [liblqr, unverified] in the
     // reference's order ((k_r r + k_g g) + k_b b); preview: RGB2LUMINANCE
     auto luma3 = [&](uint32_t c0, uint32_t c1, uint32_t c2) -> double {
-        if constexpr (DCTE_DENSE8_PROBE == 1) return (double)(c0 + c1 + c2);
         if constexpr (SEM == kSemLqr) {
             if constexpr (BPP == 1) return lut[c0];
             else return lut[c0] + lut[256 + c1] + lut[512 + c2];
@@ -1123,7 +950,7 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
     for (unsigned k = blk; k < ndirty; k += nblk) {   // uniform
         const unsigned strip = p.dirty_list[k];
         const unsigned cnt = p.tile_count[strip];
-        if (cnt <= kDenseMin<N, SEM>) continue;        // sparse (dcte_fix_strips) or gathered (fix_gather8)
+        if (cnt <= kFixDirect<N>) continue;            // sparse: dcte_fix_strips' own walk
         const unsigned tile = strip / spt;
         const int bx = (int)(tile % (unsigned)tp.tiles_x), by = (int)(tile / (unsigned)tp.tiles_x);
         const int sx0 = bx * tp.tile_w + 64 * (int)(strip % spt);
@@ -1138,9 +965,7 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
             const int gx0 = x - HL;
             const bool inside = gx0 >= 0 && gx0 + 8 <= p.w;
             // rows in batches of RB: a batch's loads are issued, then its
-            // bytes converted (liblqr: each row's first-pass step right away
-            // -- the reference's first pass runs along x for each window row,
-            // src/fft2d/shrtdct.c:62-89, so it needs that row alone)
+            // bytes converted
             constexpr int RB = DCTE_DENSE8_RB;
             double d[64];
 #pragma unroll
@@ -1158,8 +983,7 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
                     const uint32_t a = fast[rr] ? (s0 & ~3u) : 0x7ffffff0u;   // past num_records: zeros
 #pragma unroll
                     for (int j = 0; j < NW; j++)
-                        fv[rr][j] = DCTE_DENSE8_PROBE == 3 ? ((a & 4u) ? 0xffffffffu : 0u)
-                                                           : __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * j), 0, 0);
+                        fv[rr][j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * j), 0, 0);
                 }
 #pragma unroll
                 for (int rr = 0; rr < RB; rr++) {
@@ -1187,7 +1011,6 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
                             lv[c] = luma3(q8[0], BPP > 1 ? q8[1] : 0u, BPP > 1 ? q8[2] : 0u);
                         }
                     }
-                    if constexpr (SEM == kSemLqr && DCTE_DENSE8_FUSE) r64::step8(lv, 1);
                     // image row r, pixel c: liblqr data[c][r], preview data[r][c]
 #pragma unroll
                     for (int c = 0; c < 8; c++) d[SEM == kSemLqr ? c * 8 + r : r * 8 + c] = lv[c];
@@ -1195,49 +1018,14 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
             }
             double m;
             bool edge;
-            if constexpr (DCTE_DENSE8_PROBE == 2) {
-                m = 0.0;
-#pragma unroll
-                for (int i = 0; i < 64; i++) m += d[i];
-                edge = false;
-            } else if constexpr (DCTE_DENSE8_SKIP) {
-                if constexpr (!(SEM == kSemLqr && DCTE_DENSE8_FUSE)) {
-#pragma unroll
-                    for (int i = 0; i < 8; i++) {
-                        r64::step8(d + i, 8);
-                        __builtin_amdgcn_sched_barrier(0);
-                    }
-                }
-                refine8_second_skip(d, m, edge);
-            } else if constexpr (SEM == kSemLqr && DCTE_DENSE8_FUSE) {
-                refine_regs<8, DCTE_FIX_IL, false>(d, tp.ct, m, edge);
-            } else {
-                refine_regs<8>(d, tp.ct, m, edge);
-            }
+            refine_regs<8>(d, tp.ct, m, edge);
             p.out[(long long)(y - p.y0) * p.out_stride + x] =
                 edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
         }
     }
 }
 
-// The same refinement over ONE flat list: the map kernel numbered the dense
-// strips' entries consecutively (MapParams::dense_list), so wave `blk` of
-// `nblk` takes a contiguous run of 64-entry batches -- every wave gets the
-// same number of full batches whatever the strips' counts, and a batch spans
-// at most two strips (a dense strip holds more than 128 entries).  Three
-// batches are in flight per wave: batch b is transformed while batch b + 1's
-// window rows and batch b + 2's list words load.
-template <int BPP>
-struct D8Rows {
-    static constexpr int NW = (8 * BPP + 3) / 4 + 1;  // dwords of a row's 8 pixels, any alignment
-    uint32_t fv[8][NW];
-    uint32_t foff;      // 2 bits per row: byte offset of the row's first pixel in fv[r][0]
-    uint32_t fast;      // bit per row: fv holds the row (else per-pixel reads)
-    int x, y;
-    bool valid;
-};
-
-// Cursor over the flat dense list for one wave: batches of EPB entries,
+// Cursor over the flat dense list (N = 16) for one wave: batches of EPB entries,
 // the wave taking batches blk, blk + nblk, ... -- the waves resident at one
 // time work on neighbouring batches (neighbouring strips, so their window rows
 // share the L2), every wave gets the same number of full batches whatever the
@@ -1311,7 +1099,7 @@ struct DenseWalk {
 // the N = 16 map kernel a spilled register): wave k takes dense slot k and
 // writes, for every batch of EPB entries whose first entry lies in that
 // strip, {first column, first output row, strip, offset}.
-template <int EPB, bool SLOT>
+template <int EPB>
 __global__ __launch_bounds__(256) void dcte_dense_index(const TileFixParams tp)
 {
     const MapParams& p = tp.m;
@@ -1325,252 +1113,7 @@ __global__ __launch_bounds__(256) void dcte_dense_index(const TileFixParams tp)
     const uint4 di = make_uint4((unsigned)((int)(tile % (unsigned)tp.tiles_x) * tp.tile_w + 64 * (int)(strip % spt)),
                                 (unsigned)(p.y0 + (int)(tile / (unsigned)tp.tiles_x) * p.tile_h), strip, off);
     const unsigned first = (off + EPB - 1u) / EPB, last = (off + cnt - 1u) / EPB;
-    if constexpr (SLOT) {                              // gather walk: the slot alone
-        for (unsigned b = first + lane; b <= last; b += 64u) reinterpret_cast<unsigned*>(p.dense_batch)[b] = slot;
-    } else {
-        for (unsigned b = first + lane; b <= last; b += 64u) p.dense_batch[b] = di;
-    }
-}
-
-// Window I/O of the lane-per-pixel N = 8 walks (fix_dense8_flat,
-// fix_gather8): a pixel's eight image rows as whole dwords through the frame's
-// buffer resource (per-pixel reads where the window is clamped at the left /
-// right border or reaches the frame's last bytes), converted to the
-// reference's fp64 luma (liblqr LQR_ER_LUMA through the LDS tables,
-// src/render.c:315 [liblqr, unverified], in the reference's order ((k_r r +
-// k_g g) + k_b b); preview: RGB2LUMINANCE) in the window layout refine_regs
-// takes (liblqr data[dx][dy], preview data[dy][dx]).
-template <int BPP, int SEM>
-struct Win8Io {
-    static constexpr int HL = Geo<8, SEM>::HL;
-    static constexpr int NW = D8Rows<BPP>::NW;
-    const MapParams& p;
-    const double* lut;
-    uint32_t base_off;
-    unsigned nrec;
-    __amdgpu_buffer_rsrc_t rsrc;
-
-    __device__ __forceinline__ Win8Io(const MapParams& mp, const double* l) : p(mp), lut(l)
-    {
-        const uintptr_t pbase = reinterpret_cast<uintptr_t>(p.px);
-        base_off = (uint32_t)(pbase & 3u);
-        nrec = base_off + (unsigned)((long long)(p.in_rows - 1) * p.rowstride) + (unsigned)(p.w * BPP);
-        rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(pbase - base_off), (short)0, (int)nrec,
-                                                 (int)kBufFlags);
-    }
-
-    __device__ __forceinline__ double luma3(uint32_t c0, uint32_t c1, uint32_t c2) const
-    {
-        if constexpr (DCTE_DENSE8_PROBE == 1) return (double)(c0 + c1 + c2);
-        if constexpr (SEM == kSemLqr) {
-            if constexpr (BPP == 1) return lut[c0];
-            else return lut[c0] + lut[256 + c1] + lut[512 + c2];
-        } else {
-            return (double)preview_luma(c0, c1, c2, BPP);
-        }
-    }
-
-    // the window rows of list word loc of the strip at (sx0, ys) into R
-    __device__ __forceinline__ void rows(unsigned loc, int sx0, int ys, bool valid, D8Rows<BPP>& R) const
-    {
-        R.x = sx0 + (int)(loc & 63u);
-        R.y = ys + (int)(loc >> 6);
-        R.valid = valid;
-        const int gx0 = R.x - HL;
-        const bool inside = valid && gx0 >= 0 && gx0 + 8 <= p.w;
-        R.fast = 0;
-        R.foff = 0;
-#pragma unroll
-        for (int rr = 0; rr < 8; rr++) {
-            const int gy = clampi(R.y - HL + rr, 0, p.h - 1);
-            const uint32_t s0 = base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
-                                (uint32_t)(gx0 * BPP);
-            const bool fast = inside && ((s0 + 8 * BPP - 1) | 3u) < nrec;
-            R.fast |= (uint32_t)fast << rr;
-            R.foff |= (s0 & 3u) << (2 * rr);
-            const uint32_t a = fast ? (s0 & ~3u) : 0x7ffffff0u;   // past num_records: zeros
-#pragma unroll
-            for (int j = 0; j < NW; j++)
-                R.fv[rr][j] = DCTE_DENSE8_PROBE == 3 ? ((a & 4u) ? 0xffffffffu : 0u)
-                                                     : __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * j), 0, 0);
-        }
-    }
-
-    __device__ __forceinline__ void convert(const D8Rows<BPP>& R, double (&d)[64]) const
-    {
-        const int gx0 = R.x - HL;
-#pragma unroll
-        for (int r = 0; r < 8; r++) {
-            double lv[8];
-            // lanes without an entry decode their (zero) fetch like a fast row
-            if (((R.fast >> r) & 1u) || !R.valid) {
-                const uint32_t fo = (R.foff >> (2 * r)) & 3u;
-                uint32_t wd[NW - 1];
-#pragma unroll
-                for (int j = 0; j < NW - 1; j++) wd[j] = __builtin_amdgcn_alignbyte(R.fv[r][j + 1], R.fv[r][j], fo);
-#pragma unroll
-                for (int c = 0; c < 8; c++) {
-                    auto byte = [&](int b) { return (wd[b >> 2] >> (8 * (b & 3))) & 255u; };
-                    lv[c] = luma3(byte(c * BPP), BPP > 1 ? byte(c * BPP + 1) : 0u, BPP > 1 ? byte(c * BPP + 2) : 0u);
-                }
-            } else {
-                // (opaque copies: the compiler would otherwise hoist these
-                // addresses out of the rare branch into every batch)
-                int xs = gx0, yr = R.y - HL + r;
-                asm volatile("" : "+v"(xs), "+v"(yr));
-                const int gy = clampi(yr, 0, p.h - 1);
-                const uint8_t* row = p.px + (long long)(gy - p.in_row0) * p.rowstride;
-#pragma unroll
-                for (int c = 0; c < 8; c++) {
-                    const uint8_t* q8 = row + (long long)clampi(xs + c, 0, p.w - 1) * BPP;
-                    lv[c] = luma3(q8[0], BPP > 1 ? q8[1] : 0u, BPP > 1 ? q8[2] : 0u);
-                }
-            }
-            // image row r, pixel c: liblqr data[c][r], preview data[r][c]
-#pragma unroll
-            for (int c = 0; c < 8; c++) d[SEM == kSemLqr ? c * 8 + r : r * 8 + c] = lv[c];
-        }
-    }
-};
-
-template <int BPP, int SEM>
-__device__ __forceinline__ void fix_dense8_flat(const TileFixParams& tp, const double* lut,
-                                                unsigned blk, unsigned nblk)
-{
-    const MapParams& p = tp.m;
-    DenseWalk<64> dw;
-    if (!dw.init(tp, blk, nblk)) return;               // uniform
-    const unsigned b0 = dw.b0, nb = dw.nb;
-    const int lane = threadIdx.x;
-    const Win8Io<BPP, SEM> io(p, lut);
-    // batch-map entries of the next list_stage's batch b and of b + 1
-    uint4 infA = dw.info(b0), infB = b0 + 1 < nb ? dw.info(b0 + 1) : infA;
-    auto list_stage = [&](unsigned b, unsigned& loc, int& sx0, int& ys, bool& valid) {
-        const uint4 A = infA, B = infB;
-        const unsigned bn = dw.next(b);
-        if (bn < nb) {                                 // uniform
-            infA = dw.info(bn);
-            infB = bn + 1 < nb ? dw.info(bn + 1) : infA;
-        }
-        dw.list(b, A, B, (unsigned)lane, loc, sx0, ys, valid);
-    };
-    auto row_stage = [&](unsigned loc, int sx0, int ys, bool valid, D8Rows<BPP>& R) { io.rows(loc, sx0, ys, valid, R); };
-    auto convert = [&](const D8Rows<BPP>& R, double (&d)[64]) { io.convert(R, d); };
-
-    // rows one batch ahead (kPF), or loaded at their batch -- grey windows
-    // without the 24 prefetch registers fit three waves per SIMD, which the
-    // compute-bound dense grey frames prefer
-    constexpr bool kPF = BPP == 1 ? DCTE_DENSE8_PF_GREY : DCTE_DENSE8_PF;
-    unsigned locN = 0;
-    int sxN = 0, ysN = 0;
-    bool vN = false;
-    D8Rows<BPP> R;
-    {
-        unsigned loc0;
-        int sx, ys;
-        bool v;
-        list_stage(b0, loc0, sx, ys, v);
-        if (dw.next(b0) < nb) list_stage(dw.next(b0), locN, sxN, ysN, vN);
-        if constexpr (kPF) row_stage(loc0, sx, ys, v, R);
-        else { R.x = sx; R.y = ys; R.valid = v; R.fast = loc0; }   // parked: batch b0's list word
-    }
-    for (unsigned b = b0; b < nb; b = dw.next(b)) {    // uniform
-        double d[64];
-        if constexpr (!kPF) {
-            const unsigned loc = R.fast;
-            row_stage(loc, R.x, R.y, R.valid, R);
-        }
-        convert(R, d);
-        const int x = R.x, y = R.y;
-        const bool v = R.valid;
-        // the next batch's loads reuse R's registers: not above the convert
-        __builtin_amdgcn_sched_barrier(0);
-        const unsigned bn = dw.next(b);
-        if (bn < nb) {                                 // uniform
-            if constexpr (kPF) {
-                row_stage(locN, sxN, ysN, vN, R);
-            } else {
-                R.x = sxN;
-                R.y = ysN;
-                R.valid = vN;
-                R.fast = locN;
-            }
-            if (dw.next(bn) < nb) list_stage(dw.next(bn), locN, sxN, ysN, vN);
-        }
-        double m;
-        bool edge;
-        if constexpr (DCTE_DENSE8_PROBE == 2) {
-            m = 0.0;
-#pragma unroll
-            for (int i = 0; i < 64; i++) m += d[i];
-            edge = false;
-        } else {
-            refine_regs<8>(d, tp.ct, m, edge);
-        }
-        if (v)
-            p.out[(long long)(y - p.y0) * p.out_stride + x] =
-                edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
-    }
-}
-
-// The gather walk (N = 8): the small strips' entries pooled into full
-// 64-pixel batches of the flat list -- batch b's 64 entries lie in at most 64
-// consecutive slots from the batch map's first slot, so lane j loads slot
-// s0 + j and every lane finds the slot of its own entry by a binary search
-// over those offsets (shuffles), then refines its pixel like the dense walks.
-// Wave blk of nblk takes batches blk, blk + nblk, ...
-template <int BPP, int SEM>
-__device__ __forceinline__ void fix_gather8(const TileFixParams& tp, const double* lut, unsigned blk, unsigned nblk)
-{
-    const MapParams& p = tp.m;
-    const unsigned long long dc = *p.dense_ctr;
-    const unsigned nd = (unsigned)(dc >> 32), total = (unsigned)dc;
-    const unsigned spt = (unsigned)tp.tile_w / 64u, per_strip = 64u * (unsigned)p.tile_h;
-    const unsigned nstrips = (unsigned)tp.tiles_x * spt * (unsigned)((p.y1 - p.y0 + p.tile_h - 1) / p.tile_h);
-    if (nd > nstrips || total > nstrips * per_strip) return;   // uniform
-    const unsigned nb = (total + 63u) / 64u;
-    if (blk >= nb) return;                             // uniform
-    const unsigned lane = threadIdx.x;
-    const Win8Io<BPP, SEM> io(p, lut);
-    const unsigned* bslot = reinterpret_cast<const unsigned*>(p.dense_batch);
-    for (unsigned b = blk; b < nb; b += nblk) {        // uniform
-        const unsigned s0 = bslot[b];                  // slot of entry 64 b
-        const unsigned sj = s0 + lane;
-        uint2 v = make_uint2(0u, total);               // past the last slot: offset `total`
-        if (sj < nd) v = p.dense_list[sj];
-        const unsigned e = b * 64u + lane;
-        const bool valid = e < total;
-        // the last of the 64 slots whose first entry is at most e
-        int lo = 0;
-#pragma unroll
-        for (int step = 32; step > 0; step >>= 1)
-            if ((unsigned)__shfl((int)v.y, lo + step) <= e) lo += step;
-        const unsigned strip = (unsigned)__shfl((int)v.x, lo), off = (unsigned)__shfl((int)v.y, lo);
-        const unsigned loc = p.fix_list[valid ? strip * per_strip + (e - off) : 0u];
-        const unsigned tile = strip / spt;
-        const int sx0 = (int)(tile % (unsigned)tp.tiles_x) * tp.tile_w + 64 * (int)(strip % spt);
-        const int ys = p.y0 + (int)(tile / (unsigned)tp.tiles_x) * p.tile_h;
-        D8Rows<BPP> R;
-        io.rows(loc, sx0, ys, valid, R);
-        double d[64];
-        io.convert(R, d);
-        double m;
-        bool edge;
-        refine_regs<8>(d, tp.ct, m, edge);
-        if (valid)
-            p.out[(long long)(R.y - p.y0) * p.out_stride + R.x] =
-                edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
-    }
-}
-
-template <int BPP, int SEM>
-__device__ __forceinline__ void fix_dense8(const TileFixParams& tp, const double* lut, unsigned blk, unsigned nblk)
-{
-#if DCTE_FIX_FLAT
-    fix_dense8_flat<BPP, SEM>(tp, lut, blk, nblk);
-#else
-    fix_dense8_run<BPP, SEM>(tp, lut, blk, nblk);
-#endif
+    for (unsigned b = first + lane; b <= last; b += 64u) p.dense_batch[b] = di;
 }
 
 // ---- N = 16 dense strips (liblqr): four lanes per pixel ----------------
@@ -1629,9 +1172,6 @@ __device__ __forceinline__ void transpose_quad(double (&X)[4][4][4])
         }
 }
 
-#ifndef DCTE_DENSE16_PF
-#define DCTE_DENSE16_PF 1    // a batch's window lines load during the previous batch
-#endif
 template <int BPP>
 struct D16Rows {
     static constexpr int NW = (16 * BPP + 3) / 4 + 1;  // dwords of a line's 16 pixels, any alignment
@@ -1738,8 +1278,7 @@ __device__ __forceinline__ void fix_dense16_flat(const TileFixParams& tp, const 
     unsigned locN = 0;
     int sxN = 0, ysN = 0;
     bool vN = false;
-    // lines one batch ahead (DCTE_DENSE16_PF), or loaded at their batch
-    constexpr bool kPF = DCTE_DENSE16_PF;
+    // a batch's lines load during the previous batch (without: +2 %)
     D16Rows<BPP> R;
     {
         unsigned loc0;
@@ -1747,15 +1286,10 @@ __device__ __forceinline__ void fix_dense16_flat(const TileFixParams& tp, const 
         bool v;
         list16(b0, loc0, sx, ys, v);
         if (dw.next(b0) < nb) list16(dw.next(b0), locN, sxN, ysN, vN);
-        if constexpr (kPF) row_stage(loc0, sx, ys, v, R);
-        else { R.x = sx; R.y = ys; R.valid = v; R.fast = loc0; }   // parked: batch b0's list word
+        row_stage(loc0, sx, ys, v, R);
     }
     for (unsigned b = b0; b < nb; b = dw.next(b)) {    // uniform
         double X[4][4][4];
-        if constexpr (!kPF) {
-            const unsigned loc = R.fast;
-            row_stage(loc, R.x, R.y, R.valid, R);
-        }
         convert(R, X);
         const int x = R.x, y = R.y;
         const bool v = R.valid;
@@ -1763,14 +1297,7 @@ __device__ __forceinline__ void fix_dense16_flat(const TileFixParams& tp, const 
         __builtin_amdgcn_sched_barrier(0);
         const unsigned bn = dw.next(b);
         if (bn < nb) {                                 // uniform
-            if constexpr (kPF) {
-                row_stage(locN, sxN, ysN, vN, R);
-            } else {
-                R.x = sxN;
-                R.y = ysN;
-                R.valid = vN;
-                R.fast = locN;
-            }
+            row_stage(locN, sxN, ysN, vN, R);
             if (dw.next(bn) < nb) list16(dw.next(bn), locN, sxN, ysN, vN);
         }
         // first pass: the lane's four lines along the first index
@@ -1822,30 +1349,6 @@ __device__ __forceinline__ void fix_dense16_flat(const TileFixParams& tp, const 
     }
 }
 
-#ifndef DCTE_DENSE16_MINW
-#define DCTE_DENSE16_MINW 2
-#endif
-template <int BPP>
-__global__ __launch_bounds__(64, DCTE_DENSE16_MINW) void dcte_fix_dense16(const TileFixParams tp)
-{
-    __shared__ double lut[BPP == 3 ? 3 * 256 : 256];
-    fill_luma_lut<BPP == 3>(lut, threadIdx.x);
-    wave_sync_lds();
-    fix_dense16_flat<BPP>(tp, lut, blockIdx.x, gridDim.x);
-}
-
-template <int BPP, int SEM>
-__global__ __launch_bounds__(64, DCTE_DENSE8_MINW) void dcte_fix_dense8(const TileFixParams tp)
-{
-    constexpr bool kTab = SEM == kSemLqr && BPP == 3;
-    __shared__ double lut[kTab ? 3 * 256 : 256];
-    if (!DCTE_FIX_FLAT && !kGather<8, SEM> && blockIdx.x >= *tp.m.dirty_count) return;   // uniform
-    fill_luma_lut<kTab>(lut, threadIdx.x);
-    wave_sync_lds();
-    if (DCTE_FIX_FLAT || blockIdx.x < *tp.m.dirty_count) fix_dense8<BPP, SEM>(tp, lut, blockIdx.x, gridDim.x);
-    if constexpr (kGather<8, SEM>) fix_gather8<BPP, SEM>(tp, lut, blockIdx.x, gridDim.x);
-}
-
 template <int N, int BPP, int SEM>
 __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(const TileFixParams tp)
 {
@@ -1858,9 +1361,6 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
     constexpr int PDW = PB / 4;
     constexpr bool kGroup = N >= 8;                    // N lanes per pixel (else one lane)
     constexpr int PPW = kGroup ? 64 / N : 64;          // pixels per wave pass
-#ifndef DCTE_FIX_OTF
-#define DCTE_FIX_OTF 1
-#endif
     // kOtf (grey layers): window elements converted from the band's raw bytes
     // as they are read -- one byte and one table read each -- instead of a
     // staged fp64 luma band: fewer LDS bytes, more waves per CU (line art
@@ -1868,16 +1368,13 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
     // RGB keeps the staged band: three bytes, three table reads and five fp64
     // operations per element read would cost more than the occupancy wins
     // (N = 16: 1.66 -> 1.93 ms).
-#ifndef DCTE_FIX_OTF_RGB
-#define DCTE_FIX_OTF_RGB 1
-#endif
     // liblqr RGB at N = 8 reads elements from the raw band too, with the three
     // weighted quotients k_c (v / 255) tabulated so a luma is two fp64 adds
     // ((k_r r + k_g g) + k_b b, the reference's order): line art RGB 1.41 ->
     // 1.33 ms; at N = 16 the same costs +30 % (profiles/r02/fix_otf_ab.jsonl)
-    constexpr bool kTab = DCTE_FIX_OTF_RGB && SEM == kSemLqr && BPP == 3 && N == 8;
-    constexpr bool kOtf = DCTE_FIX_OTF && (BPP == 1 || kTab);
-    // dense strips go to fix_dense8* / fix_dense16_flat (kDenseOwn): no band
+    constexpr bool kTab = SEM == kSemLqr && BPP == 3 && N == 8;
+    constexpr bool kOtf = BPP == 1 || kTab;
+    // dense strips go to fix_dense8_run / fix_dense16_flat (kDenseOwn): no band
     // staging here, and the N = 16 RGB dense blocks want pre-weighted tables
     constexpr bool kOwn = kDenseOwn<N, SEM>;
     constexpr bool kTab16 = N == 16 && kOwn && BPP == 3;
@@ -1898,17 +1395,16 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
     double (*const win)[WS] = reinterpret_cast<double (*)[WS]>(rw_lds + (kOtf ? RAW_D : 0));
     const MapParams& p = tp.m;
     const unsigned ndirty = *p.dirty_count;
-    if constexpr (kOwn && DCTE_FIX_MERGE) {
+    if constexpr (kOwn) {
         // one launch for both: blocks past tp.sparse_blocks walk the dense strips
         if (blockIdx.x >= (unsigned)tp.sparse_blocks) {
             const unsigned blk = blockIdx.x - (unsigned)tp.sparse_blocks;
             const unsigned nblk = gridDim.x - (unsigned)tp.sparse_blocks;
             if constexpr (N == 8) {
-                if (!DCTE_FIX_FLAT && !kGather<N, SEM> && blk >= ndirty) return;   // uniform
+                if (blk >= ndirty) return;             // uniform
                 fill_luma_lut<kTab>(lut, threadIdx.x);
                 wave_sync_lds();
-                if (DCTE_FIX_FLAT || blk < ndirty) fix_dense8<BPP, SEM>(tp, lut, blk, nblk);
-                if constexpr (kGather<N, SEM>) fix_gather8<BPP, SEM>(tp, lut, blk, nblk);
+                fix_dense8_run<BPP, SEM>(tp, lut, blk, nblk);
             } else {
                 fill_luma_lut<kTab16>(lut, threadIdx.x);
                 wave_sync_lds();
@@ -1998,7 +1494,7 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
     // tp.sparse_blocks (the rest walk the dense strips), so they stride by
     // that many -- striding by gridDim.x skipped every strip batch past
     // sparse_blocks * SB in launches with more dirty strips than that
-    const unsigned nsparse = (kOwn && DCTE_FIX_MERGE) ? (unsigned)tp.sparse_blocks : gridDim.x;
+    const unsigned nsparse = kOwn ? (unsigned)tp.sparse_blocks : gridDim.x;
     for (unsigned k0 = blockIdx.x * SB; k0 < ndirty; k0 += nsparse * SB) {   // uniform
         const unsigned kk = k0 + sgi;
         unsigned my_strip = 0, my_cnt = 0;
@@ -2007,7 +1503,7 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
             my_cnt = p.tile_count[my_strip];
         }
         if (tp.fix_total && sl == 0 && my_cnt) atomicAdd(tp.fix_total, my_cnt);
-        const bool sparse = my_cnt <= kSparseMax<N, SEM>;
+        const bool sparse = my_cnt <= kFixDirect<N>;
         const StripGeo sg = geo(my_strip);
         const unsigned smax = wave_max_u(sparse ? my_cnt : 0u);
         if constexpr (!kGroup) {
@@ -2033,7 +1529,7 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
                     store_at(sg, lx, ly, m, edge);
                 }
             }
-        } else if constexpr (DCTE_FIX_PIPE) {
+        } else {
             // the group (GL = N lanes) takes its strip's entries one at a
             // time, software-pipelined through ONE fetch buffer: entry i's
             // bytes go to LDS first, then entry i + 1's loads (and entry
@@ -2117,44 +1613,10 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
                 lcur = lnext;
                 lnext = lafter;
             }
-        } else {
-            // the group (GL = N lanes) takes its strip's entries one at a
-            // time; lane l gathers window line l
-            const int l = sl;
-            double* d = win[sgi];
-            for (unsigned i = 0; i < smax; i++) {                         // uniform
-                const bool valid = sparse && i < my_cnt;
-                int lx = 0, ly = 0;
-                if (valid) {
-                    const unsigned loc = sg.list[i];
-                    ly = (int)(loc >> 6);
-                    lx = (int)(loc & 63);
-#pragma unroll
-                    for (int t = 0; t < N; t++) {
-                        int ox, oy;
-                        offs(t, l, ox, oy);
-                        d[t * (N + 1) + l] = luma(pixel(clampi(sg.sx0 + lx + ox - HL, 0, p.w - 1),
-                                                        clampi(sg.ys + ly + oy - HL, 0, p.h - 1)));
-                    }
-                }
-                wave_sync_lds();
-                // the group transforms its window in place (d[i][j] = d[i * (N + 1) + j])
-                if constexpr (N == 8) r64::step8(d + l, N + 1); else r64::step16(d + l, N + 1);
-                wave_sync_lds();
-                if constexpr (N == 8) r64::step8(d + (N + 1) * l, 1); else r64::step16(d + (N + 1) * l, 1);
-                wave_sync_lds();
-                double v[N];
-#pragma unroll
-                for (int c = 0; c < N; c++) v[c] = d[l * (N + 1) + c];
-                double best;
-                bool edge;
-                lastmax_group<N>(v, l, best, edge);
-                if (valid && l == 0) store_at(sg, lx, ly, best, edge);
-                wave_sync_lds();
-            }
         }
 
-        // the batch's dense strips, one at a time (N = 8: dcte_fix_dense8)
+        // the batch's dense strips, one at a time (N = 8, N = 16 liblqr: the
+        // dense walks of the extra blocks instead)
         uint64_t dense_mask = kOwn ? 0ull : __ballot(!sparse && sl == 0);
         while (dense_mask) {                                              // uniform
             const int leader = __builtin_ctzll(dense_mask);             // lane 0 of its group
@@ -2192,8 +1654,7 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
             };
             auto lum_at = [&](int r, int c) -> double {
                 if constexpr (kOtf)
-                    return DCTE_FIX_ALIGNED ? luma_px(px_at(r, c))
-                                            : luma(reinterpret_cast<const uint8_t*>(&raw[r * PDW]) + mis[r] + c * BPP);
+                    return luma_px(px_at(r, c));
                 else
                     return lum[r * LW + c];
             };
@@ -2384,7 +1845,7 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
                         double best;
                         bool edge;
                         const int rr = ly - HL - r0;
-                        if constexpr (kOtf && DCTE_FIX_ALIGNED && SEM == kSemLqr) {
+                        if constexpr (kOtf && SEM == kSemLqr) {
                             // liblqr: lane l reads window row l (contiguous bytes)
                             double lv[N];
                             line_at(rr + l, lx, lv);
@@ -2454,32 +1915,22 @@ __global__ __launch_bounds__(kFixThreads) void dcte_windows(const WinParams p)
 }
 
 // ------------------------------------------------------------------ launchers
-int map_tile_w(int n, bool wide)
+int map_tile_w(int n)
 {
-    if (wide && n == 8) return Geo<8, kSemLqr, true>::TW;
     return n == 16 ? Geo<16, kSemLqr>::TW
                    : (n == 8 ? Geo<8, kSemLqr>::TW : (n == 4 ? Geo<4, kSemLqr>::TW : Geo<2, kSemLqr>::TW));
 }
 int map_default_tile_h(int n) { return n == 16 ? DCTE_TILE_H16 : DCTE_TILE_H; }
-int map_tiles_x(int n, int w, bool wide) { return (w + map_tile_w(n, wide) - 1) / map_tile_w(n, wide); }
+int map_tiles_x(int n, int w) { return (w + map_tile_w(n) - 1) / map_tile_w(n); }
 int map_tiles_y(int n, int rows, int tile_h) { return (rows + tile_h - 1) / tile_h; }
-int map_strips_per_tile(int n, bool wide) { return n == 16 ? 1 : map_tile_w(n, wide) / 64; }
+int map_strips_per_tile(int n) { return n == 16 ? 1 : map_tile_w(n) / 64; }
 
 template <int N, int BPP, int SEM>
 static hipError_t launch_map_t(const MapParams& p, hipStream_t s)
 {
-    if constexpr (N == 8) {
-        if (p.wide) {
-            constexpr int TW = Geo<N, SEM, true>::TW;
-            dim3 grid((p.w + TW - 1) / TW, (p.y1 - p.y0 + p.tile_h - 1) / p.tile_h);
-            hipLaunchKernelGGL((dcte_map<N, BPP, SEM, true>), grid, dim3(Geo<N, SEM, true>::T), 0, s, p);
-            return hipGetLastError();
-        }
-    }
-    if (p.wide) return hipErrorInvalidValue;
     constexpr int TW = Geo<N, SEM>::TW;
     dim3 grid((p.w + TW - 1) / TW, (p.y1 - p.y0 + p.tile_h - 1) / p.tile_h);
-    hipLaunchKernelGGL((dcte_map<N, BPP, SEM, false>), grid, dim3(Geo<N, SEM>::T), 0, s, p);
+    hipLaunchKernelGGL((dcte_map<N, BPP, SEM>), grid, dim3(Geo<N, SEM>::T), 0, s, p);
     return hipGetLastError();
 }
 
@@ -2528,11 +1979,9 @@ constexpr int kMaxDevices = 64;
 template <int N, int BPP, int SEM>
 static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
 {
-    if (p.m.tile_h < 1 || p.tile_w != map_tile_w(N, p.m.wide != 0) ||
-        p.tiles_x != (p.m.w + p.tile_w - 1) / p.tile_w)
+    if (p.m.tile_h < 1 || p.tile_w != map_tile_w(N) || p.tiles_x != (p.m.w + p.tile_w - 1) / p.tile_w)
         return hipErrorInvalidValue;
-    const int nstrips = p.tiles_x * map_strips_per_tile(N, p.m.wide != 0) *
-                        ((p.m.y1 - p.m.y0 + p.m.tile_h - 1) / p.m.tile_h);
+    const int nstrips = p.tiles_x * map_strips_per_tile(N) * ((p.m.y1 - p.m.y0 + p.m.tile_h - 1) / p.m.tile_h);
     // one wave per block, as many as the device holds at once (LDS-bound:
     // ~10 per CU at N = 8 RGB); each walks the dirty list in strip batches.
     // Cached per device (CU counts may differ between devices).
@@ -2552,48 +2001,21 @@ static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
         if (dev >= 0 && dev < kMaxDevices) cache[dev].store(resident, std::memory_order_relaxed);
     }
     const int blocks = nstrips < resident ? nstrips : resident;
-    if constexpr (kFlatList<N, SEM>) {
+    if constexpr (kDenseFlat<N, SEM>) {
         // the flat list's batch map first (one wave per possible listed strip)
-        hipLaunchKernelGGL((dcte_dense_index<kDenseBatch<N>, kGather<N, SEM>>), dim3((nstrips + 3) / 4), dim3(256), 0, s,
-                           p);
+        hipLaunchKernelGGL((dcte_dense_index<kDenseBatch16>), dim3((nstrips + 3) / 4), dim3(256), 0, s, p);
         if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
     }
     if constexpr (kDenseOwn<N, SEM>) {
-        // the dense strips' walk: its own kernel (occupancy from its
-        // registers), or extra blocks of the same launch (DCTE_FIX_MERGE)
-        auto dense_kernel = [] {
-            if constexpr (N == 8) return dcte_fix_dense8<BPP, SEM>;
-            else return dcte_fix_dense16<BPP>;
-        }();
-        static std::atomic<int> dcache[kMaxDevices];
-        int dres = dev >= 0 && dev < kMaxDevices ? dcache[dev].load(std::memory_order_relaxed) : 0;
-        if (!dres) {
-            int cus = 0, per_cu = 0;
-            if (dev >= 0 &&
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dense_kernel, 64, 0) == hipSuccess &&
-                cus > 0 && per_cu > 0)
-                dres = cus * per_cu;
-            else
-                dres = 2048;
-            if (dev >= 0 && dev < kMaxDevices) dcache[dev].store(dres, std::memory_order_relaxed);
-        }
-        // flat list: up to one wave per batch the lists could hold; per-strip
-        // walk (N = 8, DCTE_FIX_FLAT=0): one per strip
-        const long long most = kFlatList<N, SEM>
-                                   ? ((long long)nstrips * 64 * p.m.tile_h + kDenseBatch<N> - 1) / kDenseBatch<N>
+        // the dense strips' walk: extra blocks of the same launch, up to one
+        // wave per batch the flat list could hold (N = 16) or per strip (N = 8)
+        const long long most = kDenseFlat<N, SEM>
+                                   ? ((long long)nstrips * 64 * p.m.tile_h + kDenseBatch16 - 1) / kDenseBatch16
                                    : nstrips;
-        const int dblocks = most < dres ? (int)most : dres;
-        if constexpr (DCTE_FIX_MERGE) {
-            TileFixParams q = p;
-            q.sparse_blocks = blocks;
-            hipLaunchKernelGGL((dcte_fix_strips<N, BPP, SEM>), dim3(blocks + dblocks), dim3(64), 0, s, q);
-            return hipGetLastError();
-        }
-        hipLaunchKernelGGL((dcte_fix_strips<N, BPP, SEM>), dim3(blocks), dim3(64), 0, s, p);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(dense_kernel, dim3(dblocks), dim3(64), 0, s, p);
+        const int dblocks = most < resident ? (int)most : resident;
+        TileFixParams q = p;
+        q.sparse_blocks = blocks;
+        hipLaunchKernelGGL((dcte_fix_strips<N, BPP, SEM>), dim3(blocks + dblocks), dim3(64), 0, s, q);
         return hipGetLastError();
     }
     hipLaunchKernelGGL((dcte_fix_strips<N, BPP, SEM>), dim3(blocks), dim3(64), 0, s, p);
@@ -2628,8 +2050,7 @@ hipError_t launch_fix_tiles(int n, int bpp, int sem, const TileFixParams& p, hip
 
 int dense_batch_entries(int n, int sem)
 {
-    if (n == 8) return kFlatList<8, kSemLqr> ? (int)kDenseBatch<8> : 0;
-    if (n == 16 && sem == kSemLqr) return kDenseFlat<16, kSemLqr> ? (int)kDenseBatch<16> : 0;
+    if (n == 16 && sem == kSemLqr) return kDenseFlat<16, kSemLqr> ? (int)kDenseBatch16 : 0;
     return 0;
 }
 

@@ -57,18 +57,6 @@ DCTE_HD void dct8_odd(float d0, float d1, float d2, float d3,
     X7 = fmaf(d3, -k8A, fmaf(d2, k8B, fmaf(d1, -k8C, d0 * k8D)));
 }
 
-// Odd outputs for the max (used inline by the *_max columns below): two
-// rotations
-//   t0 = C d0 + B d3, t3 = C d3 - B d0, t1 = D d1 + A d2, t2 = D d2 - A d1
-// give X3 = -(t3 + t1), X5 = t0 + t2, X1,7 = (P +- Q)/sqrt2 with P = t1 - t3,
-// Q = t0 - t2, and max(|P + Q|, |P - Q|) = |P| + |Q|: 14 VALU ops for the
-// four outputs instead of 16, and three values to fold instead of four.
-constexpr float k8R = 0.7071067811865475f;  // 1/sqrt2
-
-#ifndef DCTE_ODD16SC
-#define DCTE_ODD16SC 1   // N = 16 texture columns: odd half through dct16_odd_sc
-#endif
-
 // scaled-form constants (see dct8_col_sc)
 constexpr float k8rEF = 0.41421356237309503f;  // F / E = tan(pi/8)
 constexpr float k8rCB = 0.66817863791929891f;  // C / B = tan(3 pi/16)
@@ -101,80 +89,6 @@ DCTE_HD void dct8(const float x[8], float X[8])
     X[3] = fmaf(u3, k8rBA, u1) * -k8sA;
     X[5] = fmaf(u0, k8rBA, u2) * k8sA;
     X[7] = (pp - qq) * k8sPQ;
-}
-
-// max over |X[0..7]| of a column whose 8 outputs are all texture atoms,
-// folded into m.  max(|a+b|, |a-b|) = |a| + |b| replaces X0 and X4.
-DCTE_HD float dct8_tex_max(const float x[8], float m)
-{
-    float s0 = x[0] + x[7], d0 = x[0] - x[7];
-    float s1 = x[1] + x[6], d1 = x[1] - x[6];
-    float s2 = x[2] + x[5], d2 = x[2] - x[5];
-    float s3 = x[3] + x[4], d3 = x[3] - x[4];
-    float a = s0 + s3, b = s1 + s2, c = s0 - s3, e = s1 - s2;
-    float X04 = fabsf(a) + fabsf(b);
-    float X2 = fmaf(c, k8E, e * k8F);
-    float X6 = fmaf(c, k8F, -(e * k8E));
-    float t0 = fmaf(d3, k8B, d0 * k8C);
-    float t3 = fmaf(d0, -k8B, d3 * k8C);
-    float t1 = fmaf(d2, k8A, d1 * k8D);
-    float t2 = fmaf(d1, -k8A, d2 * k8D);
-    float pq = (fabsf(t1 - t3) + fabsf(t0 - t2)) * k8R;
-    m = max2in(m, X04, X2);
-    m = max2in(m, X6, pq);
-    return max2in(m, t3 + t1, t0 + t2);
-}
-
-// k1 = 1 column: X[0] is the edge atom (1,0); X[1..7] are textures.
-DCTE_HD float dct8_k1_max(const float x[8], float m, float& edge)
-{
-    float s0 = x[0] + x[7], d0 = x[0] - x[7];
-    float s1 = x[1] + x[6], d1 = x[1] - x[6];
-    float s2 = x[2] + x[5], d2 = x[2] - x[5];
-    float s3 = x[3] + x[4], d3 = x[3] - x[4];
-    float a = s0 + s3, b = s1 + s2, c = s0 - s3, e = s1 - s2;
-    edge = fabsf(a + b);
-    float X2 = fmaf(c, k8E, e * k8F);
-    float X6 = fmaf(c, k8F, -(e * k8E));
-    float t0 = fmaf(d3, k8B, d0 * k8C);
-    float t3 = fmaf(d0, -k8B, d3 * k8C);
-    float t1 = fmaf(d2, k8A, d1 * k8D);
-    float t2 = fmaf(d1, -k8A, d2 * k8D);
-    float pq = (fabsf(t1 - t3) + fabsf(t0 - t2)) * k8R;
-    m = max2in(m, a - b, X2);
-    m = max2in(m, X6, pq);
-    return max2in(m, t3 + t1, t0 + t2);
-}
-
-// A k1 >= 1 column with its outputs handed back for folding across columns
-// (Cols<8>): v[0..4] enter m_t as magnitudes -- |a| + |b| for X0/X4 (or
-// a - b = X4 alone when X0 is the edge atom C10, EDGE), X2, X6, X3, X5 --
-// and pq = |P| + |Q| = sqrt2 * max(|X1|, |X7|) goes to a chain of its own,
-// scaled by 1/sqrt2 once per pixel (rounding is monotone, so
-// max_i(pq_i) * R == max_i(pq_i * R) bit for bit).
-template <bool EDGE>
-DCTE_HD void dct8_col_parts(const float x[8], float v[5], float& pq, float& edge)
-{
-    float s0 = x[0] + x[7], d0 = x[0] - x[7];
-    float s1 = x[1] + x[6], d1 = x[1] - x[6];
-    float s2 = x[2] + x[5], d2 = x[2] - x[5];
-    float s3 = x[3] + x[4], d3 = x[3] - x[4];
-    float a = s0 + s3, b = s1 + s2, c = s0 - s3, e = s1 - s2;
-    if constexpr (EDGE) {
-        edge = fabsf(a + b);
-        v[0] = a - b;
-    } else {
-        v[0] = fabsf(a) + fabsf(b);
-    }
-    v[1] = fmaf(c, k8E, e * k8F);
-    v[2] = fmaf(c, k8F, -(e * k8E));
-    float t0 = fmaf(d3, k8B, d0 * k8C);
-    float t3 = fmaf(d0, -k8B, d3 * k8C);
-    float t1 = fmaf(d2, k8A, d1 * k8D);
-    float t2 = fmaf(d1, -k8A, d2 * k8D);
-    pq = fabsf(t1 - t3) + fabsf(t0 - t2);
-    v[3] = t3 + t1;
-    v[4] = t0 + t2;
 }
 
 // A k1 >= 1 column in SCALED form: every output magnitude is a known constant
@@ -220,7 +134,7 @@ DCTE_HD void dct8_col_sc(const float x[8], float& v1, float ye[2], float ya[2], 
 
 // k1 = 0 column in scaled form (inputs: exact integer row sums), folded into
 // the four running maxima.  The DC is never formed; X4 = (s0 - s1) + (s3 - s2)
-// as in dct8_k0_max.  X1 (the edge atom C01) = (A / sqrt2)(p + q) and
+// (exact integer partial sums).  X1 (the edge atom C01) = (A / sqrt2)(p + q) and
 // X7 = (A / sqrt2)(p - q) with p, q as in dct8_col_sc; e0 = |p + q| carries
 // the scale A / sqrt2.  25 VALU ops instead of 33.
 DCTE_HD void dct8_k0_sc(const float x[8], float& m1, float& mE, float& mA, float& mQ, float& e0)
@@ -240,37 +154,6 @@ DCTE_HD void dct8_k0_sc(const float x[8], float& m1, float& mE, float& mA, float
     float pp = fmaf(u3, -k8rBA, u1), qq = fmaf(u0, k8rBA, -u2);
     e0 = fabsf(pp + qq);
     mQ = fmaxf(mQ, fabsf(pp - qq));
-}
-
-// ten magnitudes into m: five v_max3 with abs modifiers
-DCTE_HD float fold10(float m, const float a[5], const float b[5])
-{
-    m = max2in(m, a[0], a[1]);
-    m = max2in(m, a[2], a[3]);
-    m = max2in(m, a[4], b[0]);
-    m = max2in(m, b[1], b[2]);
-    return max2in(m, b[3], b[4]);
-}
-
-// k1 = 0 column (inputs: exact integer row sums, |x| <= 5.1e6).  X[0] (the
-// DC, unused) is never formed; X4 = (s0 - s1) + (s3 - s2) avoids the large
-// partial sums a = s0 + s3, b = s1 + s2.  X[1] is the edge atom (0,1).
-DCTE_HD float dct8_k0_max(const float x[8], float m, float& edge)
-{
-    float s0 = x[0] + x[7], d0 = x[0] - x[7];
-    float s1 = x[1] + x[6], d1 = x[1] - x[6];
-    float s2 = x[2] + x[5], d2 = x[2] - x[5];
-    float s3 = x[3] + x[4], d3 = x[3] - x[4];
-    float c = s0 - s3, e = s1 - s2;
-    float X4 = (s0 - s1) + (s3 - s2);
-    float X2 = fmaf(c, k8E, e * k8F);
-    float X6 = fmaf(c, k8F, -(e * k8E));
-    float X1, X3, X5, X7;
-    dct8_odd(d0, d1, d2, d3, X1, X3, X5, X7);
-    edge = fabsf(X1);
-    m = max2in(m, X4, X2);
-    m = max2in(m, X6, X3);
-    return max2in(m, X5, X7);
 }
 
 // ---------------------------------------------------------------- N = 4, 2
@@ -307,26 +190,6 @@ constexpr float k16a5 = 0.6666556584777468f;  // cos(11 pi/32)
 constexpr float k16a6 = 0.41052452752235735f; // cos(13 pi/32)
 constexpr float k16a7 = 0.1386171691990917f;  // cos(15 pi/32)
 
-// X[2m+1] = sum_j d_j * sign * a_{|...|}; the 8 x 8 sign/index table of
-// cos(pi (2j+1)(2m+1)/32) folded onto the eight magnitudes above.
-DCTE_HD void dct16_odd(const float d[8], float X[16])
-{
-    const float A0 = k16a0, A1 = k16a1, A2 = k16a2, A3 = k16a3;
-    const float A4 = k16a4, A5 = k16a5, A6 = k16a6, A7 = k16a7;
-#define DCTE_ROW(o, c0, c1, c2, c3, c4, c5, c6, c7)                                   \
-    X[o] = fmaf(d[7], c7, fmaf(d[6], c6, fmaf(d[5], c5, fmaf(d[4], c4,                \
-           fmaf(d[3], c3, fmaf(d[2], c2, fmaf(d[1], c1, d[0] * c0)))))));
-    DCTE_ROW(1,  A0,  A1,  A2,  A3,  A4,  A5,  A6,  A7)
-    DCTE_ROW(3,  A1,  A4,  A7, -A5, -A2, -A0, -A3, -A6)
-    DCTE_ROW(5,  A2,  A7, -A3, -A1, -A6,  A4,  A0,  A5)
-    DCTE_ROW(7,  A3, -A5, -A1,  A7,  A0,  A6, -A2, -A4)
-    DCTE_ROW(9,  A4, -A2, -A6,  A0, -A7, -A1,  A5,  A3)
-    DCTE_ROW(11, A5, -A0,  A4,  A6, -A1,  A3,  A7, -A2)
-    DCTE_ROW(13, A6, -A3,  A0, -A2,  A5,  A7, -A4,  A1)
-    DCTE_ROW(15, A7, -A6,  A5, -A4,  A3, -A2,  A1, -A0)
-#undef DCTE_ROW
-}
-
 // Four odd outputs X[k0], X[k0+4], X[k0+8], X[k0+12] (k0 = 1 or 3) of the
 // 16-point transform from d_j = x_j - x_{15-j}: the rows of dct16_odd.
 DCTE_HD void dct16_odd_rows(const float d[8], int k0, float out[4])
@@ -353,46 +216,6 @@ DCTE_HD void dct16_odd_rows(const float d[8], int k0, float out[4])
 #undef DCTE_ROW
 }
 
-// Odd half of the 16-point transform (a DCT-IV of size 8) in 50 ops instead
-// of the 64 of dct16_odd: with a_j = pi (2j+1)/32,
-//   2 cos(a_j) cos(2k a_j) = cos((2k+1) a_j) + cos((2k-1) a_j),
-// so the 8-point DCT-II of d'_j = 2 cos(a_j) d_j gives Z_k = Y_k + Y_{k-1}
-// (Y_{-1} = Y_0), i.e. Y_0 = Z_0 / 2 and Y_m = Z_m - Y_{m-1}.  In hat units:
-//   X[1] = (g/2) E[0],  X[2m+1] = E[m] - X[2m-1]   (E = dct8(d')).
-constexpr float k16p0 = 1.9903694533443939f, k16p1 = 1.9138806714644176f;
-constexpr float k16p2 = 1.76384252869671f, k16p3 = 1.546020906725474f;
-constexpr float k16p4 = 1.268786568327291f, k16p5 = 0.9427934736519956f;
-constexpr float k16p6 = 0.5805693545089247f, k16p7 = 0.19603428065912154f;
-constexpr float k16h = 0.7071067811865476f;   // g / 2
-
-DCTE_HD void dct16_odd_fast(const float d[8], float X[16])
-{
-    float dp[8] = {d[0] * k16p0, d[1] * k16p1, d[2] * k16p2, d[3] * k16p3,
-                   d[4] * k16p4, d[5] * k16p5, d[6] * k16p6, d[7] * k16p7};
-    float E[8];
-    dct8(dp, E);
-    X[1] = E[0] * k16h;
-#pragma unroll
-    for (int m = 1; m < 8; m++) X[2 * m + 1] = E[m] - X[2 * m - 1];
-}
-
-// full 16-point transform: even half = 8-point transform of s_j = x_j + x_{15-j}
-// (same g), odd half from d_j = x_j - x_{15-j}.
-DCTE_HD void dct16(const float x[16], float X[16])
-{
-    float s[8], d[8], E[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        s[j] = x[j] + x[15 - j];
-        d[j] = x[j] - x[15 - j];
-    }
-    dct8(s, E);
-#pragma unroll
-    for (int m = 0; m < 8; m++) X[2 * m] = E[m];
-    dct16_odd_fast(d, X);
-}
-
-// max over the 16 outputs of an all-texture column, folded into m
 // Odd half of the 16-point transform for the max only: the DCT-IV of size 8
 // of d (X[2m+1] = sqrt2 * Y_m) through a 4-point complex DFT,
 //   v_n = d_{2n} + i d_{7-2n},  u_n = v_n exp(-i pi (4n+1)/32)      (pre-twiddle)
@@ -402,7 +225,9 @@ DCTE_HD void dct16(const float x[16], float X[16])
 // k = 1 and k = 3 are sqrt2 cos(pi/8) = E times one FMA per output (chain mE:
 // tan(pi/8) for k = 1, cot(3 pi/8) = tan(pi/8) for k = 3); k = 2 gives
 // max(|Ur + Ui|, |Ur - Ui|) = |Ur| + |Ui| at scale sqrt2 cos(pi/4) = 1
-// (chain m).  37 VALU ops instead of the 48 of dct16_odd_fast.
+// (chain m).  37 VALU ops instead of the 48 of the DCT-IV-via-DCT-II
+// recursion (X[2m+1] = E[m] - X[2m-1] over an 8-point transform of the
+// pre-scaled d, which r02 used).
 constexpr float k16c0 = 0.99518472667219693f;   // cos( 1 pi/32)
 constexpr float k16s0 = 0.098017140329560604f;  // sin( 1 pi/32)
 constexpr float k16c1 = 0.88192126434835505f;   // cos( 5 pi/32)
@@ -436,7 +261,7 @@ DCTE_HD void dct16_odd_sc(const float d[8], float& m, float& mE, float& m2, floa
     mE = max2in(mE, fmaf(u3r, k8rEF, u3i), fmaf(u3i, -k8rEF, u3r));
 }
 
-// dct16_tex_max with the even half (the 8-point transform of s, same hat
+// An all-texture column of the N = 16 second pass: the even half (the 8-point transform of s, same hat
 // units) in the scaled form of dct8_col_sc and the odd half through
 // dct16_odd_sc: magnitudes go to the running maxima m (scale 1), mE, mA, mQ
 // and m2.
@@ -455,29 +280,7 @@ DCTE_HD void dct16_tex_sc(const float x[16], float& m, float& mE, float& mA, flo
     mA = max2in(mA, ya[0], ya[1]);
     mQ = fmaxf(mQ, pq);
     m = fmaxf(m, v1);
-#if DCTE_ODD16SC
     dct16_odd_sc<false>(d, m, mE, m2);
-#else
-    float X[16];
-    dct16_odd_fast(d, X);
-#pragma unroll
-    for (int q = 1; q < 16; q += 4) m = fmaxf(fmaxf(m, fabsf(X[q])), fabsf(X[q + 2]));
-#endif
-}
-
-DCTE_HD float dct16_tex_max(const float x[16], float m)
-{
-    float s[8], d[8], X[16];
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        s[j] = x[j] + x[15 - j];
-        d[j] = x[j] - x[15 - j];
-    }
-    m = dct8_tex_max(s, m);
-    dct16_odd_fast(d, X);
-#pragma unroll
-    for (int q = 1; q < 16; q += 4) m = fmaxf(fmaxf(m, fabsf(X[q])), fabsf(X[q + 2]));
-    return m;
 }
 
 }  // namespace dcte

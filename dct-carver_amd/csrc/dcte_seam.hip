@@ -227,17 +227,21 @@ __global__ __launch_bounds__(256) void dcte_points(const SeamParams p)
 
 // Band of one carver step (dcte_carver_step): after seam s removed from a
 // frame, row y of the carved w-wide frame keeps, from column x0[y] on, `bw`
-// energies and pixels -- x0[y] = lo - R - 1 clamped to [0, max(0, w - bw)],
-// lo = min of s over rows y - R .. y + R: every pixel whose liblqr update
-// window (radius R) can reach the seam [liblqr, unverified] lies inside
-// (the seam moves <= 1 column per row, so bw = 4 R + 4 covers it).
-// One wave per row.
+// energies and pixels -- x0[y] = lo - 2R - 1 clamped to [0, max(0, w - bw)],
+// lo = min of s over rows y - 2R .. y + 2R.  The band holds every pixel
+// liblqr re-evaluates after the step (columns min s - R .. max s + R - 1 over
+// the seam rows within R [liblqr, unverified]) AND every pixel of those
+// pixels' N x N reading windows (render.c:146-152: x - (R - 1) .. x + R, rows
+// likewise), so the plug-in hook can check a callback's whole window against
+// the mirror before it serves: the seam moves <= 1 column per row, so over
+// the 4R + 1 rows that decide x0[y] it spans <= 4R columns, and bw = 8 R + 4
+// covers it.  One wave per row.
 __global__ __launch_bounds__(64) void dcte_band_gather(const BandParams p)
 {
     const int y = blockIdx.x, l = threadIdx.x;
     int lo = p.w;
-    for (int j = -p.r; j <= p.r; j++) lo = min(lo, p.seam[clamp_px(y + j, 0, p.h - 1)]);
-    const int x0 = clamp_px(lo - p.r - 1, 0, max(0, p.w - p.bw));
+    for (int j = -2 * p.r; j <= 2 * p.r; j++) lo = min(lo, p.seam[clamp_px(y + j, 0, p.h - 1)]);
+    const int x0 = clamp_px(lo - 2 * p.r - 1, 0, max(0, p.w - p.bw));
     if (l == 0) p.x0[y] = x0;
     for (int k = l; k < p.bw; k += 64) {
         const int x = min(x0 + k, p.w - 1);

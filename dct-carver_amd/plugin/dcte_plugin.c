@@ -62,6 +62,7 @@ int dcte_plugin_build_ex(dcte_map_cache *c, const uint8_t *px, int w, int h, int
         if (first && dcte_carver_create(ctx, px, w, h, bpp, rowstride, blocksize, edges, textures, ho,
                                         first, &c->mirror) == DCTE_OK) {
             c->hook_orientation = ho;
+            c->n = blocksize;
             c->mw = dcte_carver_width(c->mirror);
             c->mh = dcte_carver_height(c->mirror);
             c->bw = dcte_carver_band_width(c->mirror);
@@ -124,26 +125,60 @@ int dcte_plugin_lookup(const dcte_map_cache *c, int x, int y, int w, int h, int 
     return 0;
 }
 
-/* liblqr's LQR_ER_LUMA of a pixel [liblqr, unverified] (the formula the
- * reading window returns; src/render.c:315) */
+/* liblqr's LQR_ER_LUMA of an 8-bit pixel [liblqr, unverified] (what the
+ * reading window returns, src/render.c:315): per-channel tables of
+ * 0.2126 * (R / 255) etc., added in the formula's order -- bit-identical to
+ * evaluating it per pixel. */
+static double g_luma_tab[4][256];
+static int g_luma_tab_ready;
+
+static void luma_tables(void)
+{
+    if (g_luma_tab_ready) return;
+    for (int v = 0; v < 256; v++) {
+        g_luma_tab[0][v] = (double)v / 255;
+        g_luma_tab[1][v] = 0.2126 * ((double)v / 255);
+        g_luma_tab[2][v] = 0.7152 * ((double)v / 255);
+        g_luma_tab[3][v] = 0.0722 * ((double)v / 255);
+    }
+    g_luma_tab_ready = 1;
+}
+
 static double lqr_luma(const unsigned char *q, int bpp)
 {
-    if (bpp == 1) return (double)q[0] / 255;
-    return 0.2126 * ((double)q[0] / 255) + 0.7152 * ((double)q[1] / 255) +
-           0.0722 * ((double)q[2] / 255);
+    if (bpp == 1) return g_luma_tab[0][q[0]];
+    return g_luma_tab[1][q[0]] + g_luma_tab[2][q[1]] + g_luma_tab[3][q[2]];
+}
+
+static int clamp_int(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
+
+int dcte_plugin_window_check(const dcte_map_cache *c, int x, int y, int w, int h,
+                             double *const *data)
+{
+    if (!c || !c->band_valid || !data || w != c->mw || h != c->mh) return 0;
+    luma_tables();
+    const int r = c->n / 2;
+    for (int i = -r + 1; i <= r; i++) {         /* the reference's gather order, render.c:146-152 */
+        const int xx = clamp_int(x + i, 0, w - 1);
+        const double *line = data[i + r - 1];
+        for (int j = -r + 1; j <= r; j++) {
+            const int yy = clamp_int(y + j, 0, h - 1);
+            const int k = xx - c->band_x0[yy];
+            if (k < 0 || k >= c->bw) return 0;
+            const double l = lqr_luma(c->band_px + ((size_t)yy * c->bw + (size_t)k) * c->bpp, c->bpp);
+            if (!(fabs(l - line[j + r - 1]) <= 1e-9)) return -1;
+        }
+    }
+    return 1;
 }
 
 int dcte_plugin_lookup_hook(dcte_map_cache *c, int x, int y, int w, int h, int orientation,
-                            double center_luma, float *out)
+                            double *const *data, float *out)
 {
-    if (dcte_plugin_lookup(c, x, y, w, h, orientation, out)) {
-        if (c) c->served_map++;
-        return 1;
-    }
-    if (!c || !c->valid || !c->hook_ok || orientation != c->hook_orientation || h != c->mh ||
-        x < 0 || y < 0 || x >= w || y >= h)
+    if (!c || !c->valid || !c->hook_ok || !data || orientation != c->hook_orientation ||
+        h != c->mh || x < 0 || y < 0 || x >= w || y >= h)
         return 0;
-    /* liblqr carved since the mirror's last step: carve the same seams */
+    /* liblqr carved since the mirror's last step: carve as many seams */
     while (w < c->mw) {
         if (dcte_carver_step(c->mirror, NULL, c->band_x0, c->band_e, c->band_px) != DCTE_OK) {
             release_hook(c);
@@ -154,18 +189,18 @@ int dcte_plugin_lookup_hook(dcte_map_cache *c, int x, int y, int w, int h, int o
         c->steps++;
         c->band_valid = 1;
     }
-    const int k = x - c->band_x0[y];
-    if (w != c->mw || !c->band_valid || k < 0 || k >= c->bw) {
+    const int k = x - (c->band_valid && w == c->mw ? c->band_x0[y] : 0);
+    const int chk = k >= 0 && k < c->bw ? dcte_plugin_window_check(c, x, y, w, h, data) : 0;
+    if (chk <= 0) {
+        /* a window that differs from the mirror, or reaches past a band that
+         * holds every window of liblqr's update region while the two carve the
+         * same seams: the mirror no longer follows liblqr's image */
+        if (chk == 0) c->out_of_band++;
+        release_hook(c);
         c->missed++;
         return 0;
     }
-    const size_t at = (size_t)y * c->bw + (size_t)k;
-    if (!isnan(center_luma) && fabs(lqr_luma(c->band_px + at * c->bpp, c->bpp) - center_luma) > 1e-9) {
-        release_hook(c);       /* the mirror diverged from liblqr's image */
-        c->missed++;
-        return 0;
-    }
-    *out = c->band_e[at];
+    *out = c->band_e[(size_t)y * c->bw + (size_t)k];
     c->served_band++;
     return 1;
 }

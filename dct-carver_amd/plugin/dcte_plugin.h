@@ -31,16 +31,19 @@ typedef struct {
     int status;      /* DCTE_* code of the last build */
     /* opt-in seam hook (DCTE_PLUGIN_SEAM_HOOK): a device
      * mirror of the carver that replays each seam liblqr carves and hands
-     * back the energies around it, so update_emap's callbacks are served too */
+     * back the energies and pixels around it, so update_emap's callbacks are
+     * served too -- each only after the callback's whole reading window
+     * matched the mirror's pixels */
     struct dcte_carver *mirror;
     int hook_orientation;  /* the orientation liblqr resizes in */
     int hook_ok;           /* 0 once the mirror lost track of liblqr's image */
+    int n;                 /* blocksize: the window is n x n, radius n / 2 */
     int mw, mh, bpp, bw;   /* mirror's current width, height; bytes per pixel; band width */
     int band_valid;
     int *band_x0;          /* mh: first band column per row */
     float *band_e;         /* mh x bw energies of the last step's band */
-    unsigned char *band_px;/* mh x bw x bpp pixels (divergence check) */
-    long long served_map, served_band, missed, steps;
+    unsigned char *band_px;/* mh x bw x bpp pixels of the carved frame (window check) */
+    long long served_band, missed, out_of_band, steps;
 } dcte_map_cache;
 
 #define DCTE_PLUGIN_SEAM_HOOK 1u
@@ -69,16 +72,30 @@ int dcte_plugin_build_ex(dcte_map_cache *c, const uint8_t *px, int w, int h, int
 int dcte_plugin_lookup(const dcte_map_cache *c, int x, int y, int w, int h,
                        int orientation, float *out);
 
-/* The same, plus the seam hook: when the carver has become narrower than the
- * mirror (liblqr carved a seam), the mirror carves the same seam on the GPU
- * and pixels of its update band are served too.  center_luma: what the
- * callback's reading window holds at offset (0, 0) (lqr_rwindow_read, as
- * src/render.c:150 reads it), checked against the mirror's pixel; a mismatch
- * means the mirror no longer follows liblqr's image and switches the hook off
- * for this carver (NaN skips the check).  Misses return 0: the callback then
- * runs its original per-window code. */
+/* The seam hook, for the callbacks dcte_plugin_lookup misses: when the
+ * carver has become narrower than the mirror (liblqr carved a seam), the
+ * mirror carves its own seam on the GPU and pixels of its update band are
+ * served.  `data` is the window the callback's original body has just
+ * gathered -- params->data, data[i + r - 1][j + r - 1] = lqr_rwindow_read of
+ * the clamped offsets (i, j), i, j in [-(r - 1), r], r = n / 2
+ * (src/render.c:141-152).  A value is served only when EVERY element of that
+ * window equals liblqr's luma of the mirror's pixel at the same clamped
+ * position (|difference| <= 1e-9: distinct 8-bit lumas differ by >= 7.8e-7),
+ * so the served energy is the energy of exactly the window the original body
+ * would transform, whatever seam liblqr picked.  A window that differs from
+ * the mirror, or has a pixel outside the band (which holds every window of
+ * liblqr's update region while the two carve the same seams), means the
+ * mirror no longer follows liblqr's image: the hook misses and switches
+ * itself off for this carver.  Misses return 0: the callback then runs its
+ * original transform. */
 int dcte_plugin_lookup_hook(dcte_map_cache *c, int x, int y, int w, int h, int orientation,
-                            double center_luma, float *out);
+                            double *const *data, float *out);
+
+/* The window test of dcte_plugin_lookup_hook alone, on the current band: 1 =
+ * every element matches the mirror, 0 = a window pixel lies outside the band
+ * (or no band), -1 = an element differs.  Exposed for tests. */
+int dcte_plugin_window_check(const dcte_map_cache *c, int x, int y, int w, int h,
+                             double *const *data);
 
 void dcte_plugin_release(dcte_map_cache *c);
 

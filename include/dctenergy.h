@@ -92,12 +92,6 @@ extern "C" {
                                again band-wise and keep that stream band-wise.
                                Setting this option re-enables the single
                                launch. */
-#define DCTE_OPT_WIDE_BANDS 8 /* N = 8 launches of at most two rounds of map
-                               workgroups (a strong-scaling rank's band): 1 =
-                               1024-thread lockstep tiles, 0 = the ordinary
-                               256-thread tiles with falling wave priority
-                               (default: faster per band).  Results do not
-                               depend on it. */
 #define DCTE_OPT_TSTAMP_BUF 7 /* diagnostic, timing-probe builds (DCTE_TSTAMP=1)
                                only: device address of a buffer of 3 uint64
                                per map workgroup {start, end, HW_ID}; 0 = none.
@@ -257,7 +251,8 @@ int dcte_carve(dcte_ctx *ctx, const uint8_t *px, int w, int h, int bpp, size_t r
  * (dcte_seam_carve_device), then hands back the energies -- and the pixels,
  * so the caller can check that it follows liblqr's image -- of a band around
  * the seam: row y holds band_width columns from band_x0[y] on of the carved
- * frame, covering every pixel whose radius-N/2 window reaches the seam.
+ * frame, covering every pixel whose radius-N/2 window reaches the seam and
+ * every pixel of those pixels' own N x N windows (the hook checks them).
  * Every value equals dcte_energy_map of the carved frame at that pixel.
  * liblqr semantics (DCTE_LQR), bpp 1 or 3.
  *
@@ -275,7 +270,7 @@ int dcte_carver_create(dcte_ctx *ctx, const uint8_t *px, int w, int h, int bpp, 
 int dcte_carver_step(dcte_carver *c, int *seam, int *band_x0, float *band_e, uint8_t *band_px);
 int dcte_carver_width(const dcte_carver *c);       /* current width of the mirrored frame */
 int dcte_carver_height(const dcte_carver *c);
-int dcte_carver_band_width(const dcte_carver *c);  /* 2 N + 4 */
+int dcte_carver_band_width(const dcte_carver *c);  /* 4 N + 4 */
 void dcte_carver_destroy(dcte_carver *c);
 
 /* ---- energy image as 8-bit grey ----------------------

@@ -37,13 +37,25 @@ static double lqr_rwindow_read(LqrReadingWindow *rw, int dx, int dy, int ch)
 typedef struct {
     float edges, textures;
     int blocksize;
+    double d[256];       /* params->data: the gathered window, data[dx][dy] */
+    double *rows[16];    /* its row pointers (alloc_2d_double layout) */
     dcte_map_cache gpu;
 } EnergyParameters;
+
+static void params_init(EnergyParameters *p, float edges, float textures, int n)
+{
+    memset(p, 0, sizeof(*p));
+    p->edges = edges;
+    p->textures = textures;
+    p->blocksize = n;
+    for (int i = 0; i < n; i++) p->rows[i] = p->d + i * n;
+}
 
 float orc_window_energy(int n, const double *win, float edges, float textures); /* oracle */
 int orc_seam_find(const float *E, long long stride, int w, int h, int *seam, float *M); /* oracle */
 
-static long long g_fallback_calls;
+static long long g_fallback_calls, g_served_map, g_verified, g_bad;
+static int g_verify;      /* re-run the original body on every hook-served callback */
 
 static int clamp_offset_to_border(int base, int offset, int lo, int hi)
 {
@@ -52,20 +64,30 @@ static int clamp_offset_to_border(int base, int offset, int lo, int hi)
     return offset;
 }
 
-/* the reference callback body (src/render.c:134-157) */
-static float original_dct_pixel_energy(int x, int y, int w, int h, LqrReadingWindow *rw, void *extra)
+/* the reference callback body (src/render.c:134-157), first half: the gather */
+static void gather_window(int x, int y, int w, int h, LqrReadingWindow *rw, EnergyParameters *p)
 {
-    EnergyParameters *p = (EnergyParameters *)extra;
-    int r = lqr_rwindow_get_radius(rw), n = p->blocksize;
-    double d[256];
+    int r = lqr_rwindow_get_radius(rw);
     for (int i = -r + 1; i <= r; i++)
         for (int j = -r + 1; j <= r; j++) {
             int ii = clamp_offset_to_border(x, i, 0, w - 1);
             int jj = clamp_offset_to_border(y, j, 0, h - 1);
-            d[(i + r - 1) * n + (j + r - 1)] = lqr_rwindow_read(rw, ii, jj, 0);
+            p->rows[i + r - 1][j + r - 1] = lqr_rwindow_read(rw, ii, jj, 0);
         }
+}
+
+/* second half: dctNxN + weighted_max_dct_correlation (the oracle plays them) */
+static float window_energy(const EnergyParameters *p)
+{
+    return orc_window_energy(p->blocksize, p->d, p->edges, p->textures);
+}
+
+static float original_dct_pixel_energy(int x, int y, int w, int h, LqrReadingWindow *rw, void *extra)
+{
+    EnergyParameters *p = (EnergyParameters *)extra;
+    gather_window(x, y, w, h, rw, p);
     g_fallback_calls++;
-    return orc_window_energy(n, d, p->edges, p->textures);
+    return window_energy(p);
 }
 
 static int g_orientation; /* lqr_carver_get_orientation of the fake carver */
@@ -76,13 +98,22 @@ static float dct_pixel_energy(int x, int y, int w, int h, LqrReadingWindow *rw, 
 {
     EnergyParameters *p = (EnergyParameters *)extra;
     float v;
-    if (g_use_hook) {
-        if (dcte_plugin_lookup_hook(&p->gpu, x, y, w, h, g_orientation, lqr_rwindow_read(rw, 0, 0, 0), &v))
-            return v;
-    } else if (dcte_plugin_lookup(&p->gpu, x, y, w, h, g_orientation, &v)) {
+    if (dcte_plugin_lookup(&p->gpu, x, y, w, h, g_orientation, &v)) {
+        g_served_map++;
         return v;
     }
-    return original_dct_pixel_energy(x, y, w, h, rw, extra);
+    if (!g_use_hook) return original_dct_pixel_energy(x, y, w, h, rw, extra);
+    gather_window(x, y, w, h, rw, p);
+    if (dcte_plugin_lookup_hook(&p->gpu, x, y, w, h, g_orientation, p->rows, &v)) {
+        if (g_verify) {  /* test mode: what the original body returns for this window */
+            const float ref = window_energy(p);
+            g_verified++;
+            if (!(fabsf(v - ref) <= 1e-5f * fabsf(ref) + 1e-9f)) g_bad++;
+        }
+        return v;
+    }
+    g_fallback_calls++;
+    return window_energy(p);
 }
 
 /* Carver built on px (w x h, bpp), energy function registered with radius
@@ -104,7 +135,8 @@ int fake_build_emap(const uint8_t *px, int w, int h, int bpp, int n, float edges
             luma[(size_t)y * w + x] = bpp == 1 ? (double)q[0] / 255
                 : 0.2126 * ((double)q[0] / 255) + 0.7152 * ((double)q[1] / 255) + 0.0722 * ((double)q[2] / 255);
         }
-    EnergyParameters p = {edges, textures, n, {0}};
+    EnergyParameters p;
+    params_init(&p, edges, textures, n);
     *gpu_status = use_gpu ? dcte_plugin_build(&p.gpu, px, w, h, bpp, (size_t)w * bpp, n, edges,
                                               textures, transposed)
                           : DCTE_ENODEV;
@@ -123,7 +155,7 @@ int fake_build_emap(const uint8_t *px, int w, int h, int bpp, int n, float edges
         for (int y = 0; y < fh; y++)
             for (int x = 0; x < cw; x++) cur[(size_t)y * cw + x] = fr[(size_t)y * fw + x];
     }
-    g_fallback_calls = 0;
+    g_fallback_calls = g_served_map = 0;
     g_orientation = transposed;
     LqrReadingWindow rw = {cur, cw, fh, 0, 0, n / 2};
     for (int y = 0; y < fh; y++)
@@ -140,6 +172,148 @@ int fake_build_emap(const uint8_t *px, int w, int h, int bpp, int n, float edges
     return 0;
 }
 
+/* A DP that breaks ties the other way: the same recursion as orc_seam_find
+ * (oracle/dcte_oracle.c), but the RIGHTMOST minimum wins among the parent
+ * candidates and in the last row.  Stands in for a liblqr whose seam differs
+ * from the mirror's on equal energies. */
+static void seam_find_rightmost(const float *E, int w, int h, int *seam)
+{
+    float *prev = (float *)malloc(sizeof(float) * (size_t)w), *cur = (float *)malloc(sizeof(float) * (size_t)w);
+    signed char *par = (signed char *)malloc((size_t)w * h);
+    for (int x = 0; x < w; x++) prev[x] = E[x];
+    for (int y = 1; y < h; y++) {
+        for (int x = 0; x < w; x++) {
+            int lo = x > 0 ? x - 1 : 0, hi = x < w - 1 ? x + 1 : w - 1, arg = lo;
+            for (int c = lo + 1; c <= hi; c++)
+                if (prev[c] <= prev[arg]) arg = c;
+            cur[x] = E[(size_t)y * w + x] + prev[arg];
+            par[(size_t)y * w + x] = (signed char)(arg - x);
+        }
+        float *t = prev;
+        prev = cur;
+        cur = t;
+    }
+    int x = 0;
+    for (int c = 1; c < w; c++)
+        if (prev[c] <= prev[x]) x = c;
+    seam[h - 1] = x;
+    for (int y = h - 1; y > 0; y--) {
+        x += par[(size_t)y * w + x];
+        seam[y - 1] = x;
+    }
+    free(prev);
+    free(cur);
+    free(par);
+}
+
+/* Shift the seam by one column in one row (the first row from the middle
+ * down where the seam stays connected and inside the frame). */
+static void seam_shift_one_row(int *s, int w, int h)
+{
+    for (int k = 0; k < h; k++) {
+        const int y = (h / 2 + k) % h;
+        for (int d = 1; d >= -1; d -= 2) {
+            const int v = s[y] + d;
+            if (v < 0 || v >= w) continue;
+            if (y > 0 && abs(v - s[y - 1]) > 1) continue;
+            if (y < h - 1 && abs(v - s[y + 1]) > 1) continue;
+            s[y] = v;
+            return;
+        }
+    }
+}
+
+/* Self-test of the hook's window check on the host (no device): a synthetic
+ * cache over a random w x h luma frame with a band around a fixed seam.
+ * Returns 0 when (1) every window of the band's update pixels matches, (2) a
+ * window with any one element off by one 8-bit luma step is rejected (-1) and
+ * (3) windows reaching past the band miss (0); else the failing case's code. */
+int fake_window_check_selftest(int n, int bpp, unsigned seed)
+{
+    const int w = 61, h = 23, r = n / 2, bw = 8 * r + 4;
+    unsigned char *px = (unsigned char *)malloc((size_t)w * h * bpp);
+    double *luma = (double *)malloc(sizeof(double) * (size_t)w * h);
+    int *x0 = (int *)malloc(sizeof(int) * h);
+    unsigned char *bpx = (unsigned char *)malloc((size_t)h * bw * bpp);
+    int rc = 0;
+    for (size_t i = 0; i < (size_t)w * h * bpp; i++) {
+        seed = seed * 1664525u + 1013904223u;
+        px[i] = (unsigned char)(seed >> 24);
+    }
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            const unsigned char *q = px + ((size_t)y * w + x) * bpp;
+            luma[(size_t)y * w + x] = bpp == 1 ? (double)q[0] / 255
+                : 0.2126 * ((double)q[0] / 255) + 0.7152 * ((double)q[1] / 255) + 0.0722 * ((double)q[2] / 255);
+        }
+    /* a seam wandering around column 30; band rows as dcte_band_gather builds them */
+    int s[23];
+    for (int y = 0; y < h; y++) s[y] = 30 + (y % 5 < 3 ? y % 5 : 5 - y % 5);
+    for (int y = 0; y < h; y++) {
+        int lo = w;
+        for (int j = -2 * r; j <= 2 * r; j++) {
+            const int yy = y + j < 0 ? 0 : y + j >= h ? h - 1 : y + j;
+            if (s[yy] < lo) lo = s[yy];
+        }
+        int a = lo - 2 * r - 1, mx = w - bw > 0 ? w - bw : 0;
+        x0[y] = a < 0 ? 0 : a > mx ? mx : a;
+        for (int k = 0; k < bw; k++) {
+            const int x = x0[y] + k < w - 1 ? x0[y] + k : w - 1;
+            memcpy(bpx + ((size_t)y * bw + k) * bpp, px + ((size_t)y * w + x) * bpp, bpp);
+        }
+    }
+    dcte_map_cache c;
+    memset(&c, 0, sizeof(c));
+    c.n = n;
+    c.mw = w;
+    c.mh = h;
+    c.bpp = bpp;
+    c.bw = bw;
+    c.band_valid = 1;
+    c.band_x0 = x0;
+    c.band_px = bpx;
+    EnergyParameters p;
+    params_init(&p, 0.3f, 0.7f, n);
+    LqrReadingWindow rw = {luma, w, h, 0, 0, r};
+    long long checked = 0;
+    for (int y = 0; y < h && !rc; y++) {
+        int a = w, b = -1;  /* update columns of row y (fake_resize's rule) */
+        for (int y1 = y - r; y1 <= y + r; y1++) {
+            if (y1 < 0 || y1 >= h) continue;
+            if (s[y1] - r < a) a = s[y1] - r;
+            if (s[y1] + r - 1 > b) b = s[y1] + r - 1;
+        }
+        if (a < 0) a = 0;
+        if (b > w - 1) b = w - 1;
+        for (int x = a; x <= b && !rc; x++) {
+            rw.x = x;
+            rw.y = y;
+            gather_window(x, y, w, h, &rw, &p);
+            if (dcte_plugin_window_check(&c, x, y, w, h, p.rows) != 1) rc = 1;
+            for (int e = 0; e < n * n && !rc; e += 7) {   /* one element off by one luma step */
+                const double keep = p.d[e];
+                p.d[e] = keep + (bpp == 1 ? 1.0 / 255 : 0.0722 / 255);
+                if (dcte_plugin_window_check(&c, x, y, w, h, p.rows) != -1) rc = 2;
+                p.d[e] = keep;
+            }
+            checked++;
+        }
+    }
+    /* a pixel far left of the band: its window leaves it */
+    if (!rc) {
+        rw.x = 0;
+        rw.y = h / 2;
+        gather_window(0, h / 2, w, h, &rw, &p);
+        if (x0[h / 2] > 0 && dcte_plugin_window_check(&c, 0, h / 2, w, h, p.rows) != 0) rc = 3;
+    }
+    if (!rc && checked == 0) rc = 4;
+    free(px);
+    free(luma);
+    free(x0);
+    free(bpx);
+    return rc;
+}
+
 /* liblqr's resize loop for the plug-in's carver (lqr_carver_resize,
  * src/render.c:377; carver set up with delta_x 1, rigidity 0 at
  * src/render.c:313) [liblqr, unverified]: the energy build (one callback per
@@ -153,15 +327,21 @@ int fake_build_emap(const uint8_t *px, int w, int h, int bpp, int n, float edges
  * The plug-in is built on px as in init_carver_from_vals; `hook` selects the
  * patched callback with the seam hook (DCTE_PLUGIN_SEAM_HOOK).  Outputs: the
  * final energies (fh x cw), the final image bytes (fh x cw x bpp), the seams
- * (seams x fh) and counts[6] = {callbacks, fallback (original code),
+ * (seams x fh) and counts[10] = {callbacks, fallback (original transform),
  * served from a map, served from a seam band, mirror steps, nanoseconds spent
- * in the update_emap callbacks (incl. the mirror's steps)}.
+ * in the update_emap callbacks (incl. the mirror's steps), hook-served values
+ * re-checked against the original body (verify), of those off tolerance,
+ * hook misses, hook still on at the end}.
  * transposed: vertical resize -- the carver works on the transposed frame.
- * perturb (test of the hook's divergence check): after the build, liblqr's
- * image differs slightly from the frame the plug-in was given. */
+ * diverge (tests of the hook's window check): 0 = liblqr follows the
+ * mirror's rules; 1 = after the build liblqr's image differs slightly from
+ * the frame the plug-in was given (+1e-3 luma); 2 = every seam liblqr carves
+ * is shifted by one column in one row; 3 = liblqr's DP takes the rightmost
+ * minimum on ties (seam_find_rightmost).  verify: re-run the original body on
+ * every hook-served callback and count values off the parity tolerance. */
 int fake_resize(const uint8_t *px, int w, int h, int bpp, int n, float edges, float textures,
-                int use_gpu, int hook, int seams, int transposed, int perturb, float *out_emap,
-                uint8_t *out_px, int *out_seams, long long *counts, int *gpu_status)
+                int use_gpu, int hook, int seams, int transposed, int diverge, int verify,
+                float *out_emap, uint8_t *out_px, int *out_seams, long long *counts, int *gpu_status)
 {
     const int fw = transposed ? h : w, fh = transposed ? w : h;
     if (seams < 0 || seams >= fw) return -1;
@@ -178,13 +358,15 @@ int fake_resize(const uint8_t *px, int w, int h, int bpp, int n, float edges, fl
             luma[(size_t)y * fw + x] = bpp == 1 ? (double)q[0] / 255
                 : 0.2126 * ((double)q[0] / 255) + 0.7152 * ((double)q[1] / 255) + 0.0722 * ((double)q[2] / 255);
         }
-    EnergyParameters p = {edges, textures, n, {0}};
+    EnergyParameters p;
+    params_init(&p, edges, textures, n);
     *gpu_status = use_gpu ? dcte_plugin_build_ex(&p.gpu, px, w, h, bpp, (size_t)w * bpp, n, edges,
                                                  textures, transposed, hook ? DCTE_PLUGIN_SEAM_HOOK : 0u)
                           : DCTE_ENODEV;
-    g_fallback_calls = 0;
+    g_fallback_calls = g_served_map = g_verified = g_bad = 0;
     g_orientation = transposed;
     g_use_hook = hook;
+    g_verify = verify;
     long long calls = 0, update_ns = 0;
     int cw = fw;
     const int r = n / 2;
@@ -196,10 +378,12 @@ int fake_resize(const uint8_t *px, int w, int h, int bpp, int n, float edges, fl
             emap[(size_t)y * cw + x] = dct_pixel_energy(x, y, cw, fh, &rw, &p);
             calls++;
         }
-    if (perturb)
+    if (diverge == 1)
         for (size_t i = 0; i < (size_t)cw * fh; i++) luma[i] += 1e-3;
     for (int k = 0; k < seams; k++) {
-        orc_seam_find(emap, cw, cw, fh, s, NULL);
+        if (diverge == 3) seam_find_rightmost(emap, cw, fh, s);
+        else orc_seam_find(emap, cw, cw, fh, s, NULL);
+        if (diverge == 2) seam_shift_one_row(s, cw, fh);
         if (out_seams) memcpy(out_seams + (size_t)k * fh, s, sizeof(int) * (size_t)fh);
         /* carve: compact every row to cw - 1 (row stride follows the width) */
         for (int y = 0; y < fh; y++) {
@@ -242,12 +426,16 @@ int fake_resize(const uint8_t *px, int w, int h, int bpp, int n, float edges, fl
     if (out_px) memcpy(out_px, img, (size_t)cw * fh * bpp);
     counts[0] = calls;
     counts[1] = g_fallback_calls;
-    counts[2] = p.gpu.served_map;
+    counts[2] = g_served_map;
     counts[3] = p.gpu.served_band;
     counts[4] = p.gpu.steps;
     counts[5] = update_ns;
+    counts[6] = g_verified;
+    counts[7] = g_bad;
+    counts[8] = p.gpu.missed;
+    counts[9] = p.gpu.hook_ok;
     dcte_plugin_release(&p.gpu);
-    g_use_hook = 0;
+    g_use_hook = g_verify = 0;
     free(img);
     free(luma);
     free(emap);

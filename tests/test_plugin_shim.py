@@ -40,8 +40,10 @@ def fake():
         L.fake_resize.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                   ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_int,
                                   ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                   ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_int)]
+        L.fake_window_check_selftest.restype = ctypes.c_int
+        L.fake_window_check_selftest.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint]
         _lib = L
     return _lib
 
@@ -60,9 +62,14 @@ def build_emap(img, n, e, t, use_gpu, removed=0, transposed=False):
     return out, calls.value, status.value
 
 
-def resize(img, n, e, t, seams, use_gpu, hook, transposed=False, perturb=False):
+DIVERGE = {"none": 0, "perturb": 1, "shift_row": 2, "rightmost_ties": 3}
+
+
+def resize(img, n, e, t, seams, use_gpu, hook, transposed=False, diverge="none", verify=False):
     """fake liblqr resize loop (tests/fake_lqr: energy build, then per seam DP,
-    carve, update_emap through the patched callback) -> dict."""
+    carve, update_emap through the patched callback) -> dict.  diverge: how
+    the fake liblqr departs from the mirror (fake_resize's doc); verify: the
+    original body re-run on every hook-served callback ("verified", "bad")."""
     img = np.ascontiguousarray(img)
     h, w = img.shape[:2]
     bpp = 1 if img.ndim == 2 else img.shape[2]
@@ -70,16 +77,28 @@ def resize(img, n, e, t, seams, use_gpu, hook, transposed=False, perturb=False):
     emap = np.empty((fh, fw - seams), np.float32)
     px = np.empty((fh, fw - seams) + img.shape[2:], np.uint8)
     seam_cols = np.empty((max(seams, 1), fh), np.int32)
-    counts = (ctypes.c_longlong * 6)()
+    counts = (ctypes.c_longlong * 10)()
     status = ctypes.c_int()
     rc = fake().fake_resize(img.ctypes.data, w, h, bpp, n, e, t, int(use_gpu), int(hook), seams,
-                            int(transposed), int(perturb), emap.ctypes.data, px.ctypes.data,
-                            seam_cols.ctypes.data, counts, ctypes.byref(status))
+                            int(transposed), DIVERGE[diverge], int(verify), emap.ctypes.data,
+                            px.ctypes.data, seam_cols.ctypes.data, counts, ctypes.byref(status))
     assert rc == 0
     c = list(counts)
     return {"emap": emap, "px": px, "seams": seam_cols[:seams], "callbacks": c[0],
             "fallback": c[1], "served_map": c[2], "served_band": c[3], "steps": c[4], "update_ns": c[5],
+            "verified": c[6], "bad": c[7], "missed": c[8], "hook_on": c[9],
             "status": status.value, "initial": fw * fh}
+
+
+@pytest.mark.parametrize("n", [2, 4, 8, 16])
+@pytest.mark.parametrize("bpp", [1, 3])
+def test_hook_window_check(n, bpp):
+    """The hook's window test on the host (no device): over a synthetic band
+    around a wandering seam, every update pixel's gathered window matches the
+    band, the same window with any one element moved by one 8-bit luma step
+    is rejected, and a window past the band misses."""
+    for seed in (1, 2, 3):
+        assert fake().fake_window_check_selftest(n, bpp, seed) == 0
 
 
 def test_resize_loop_without_gpu_is_the_reference():
@@ -91,7 +110,8 @@ def test_resize_loop_without_gpu_is_the_reference():
         pytest.skip("device visible; covered by the GPU test")
     img = load_input("natural_rgb_73x59.npy")
     for n, transposed in ((8, False), (4, True), (16, False)):
-        r = resize(img, n, 0.15, 0.85, 6, use_gpu=True, hook=True, transposed=transposed)
+        r = resize(img, n, 0.15, 0.85, 6, use_gpu=True, hook=True, transposed=transposed,
+                   verify=True)
         assert r["status"] == dctenergy.DCTE_ENODEV
         assert r["fallback"] == r["callbacks"] > r["initial"]
         assert r["served_map"] == r["served_band"] == r["steps"] == 0
@@ -103,35 +123,46 @@ def test_resize_loop_without_gpu_is_the_reference():
 def test_seam_hook_serves_update_emap(n, transposed):
     """The update_emap hook: with it every callback of a
     liblqr resize -- the build and every seam's update band -- is answered by
-    the GPU (no per-window fallback), and the energies liblqr ends with are
-    bit-identical to the GPU map of the carved image (within tolerance of the
-    reference); without it only the build is served."""
+    the GPU (no per-window transform), every served value equals what the
+    original body returns for the same window (re-run on each), and the
+    energies liblqr ends with are bit-identical to the GPU map of the carved
+    image; without it only the build is served."""
     img = load_input("natural_rgb_97x41.npy")
     seams = 9
     plain = resize(img, n, 0.15, 0.85, seams, use_gpu=True, hook=False, transposed=transposed)
-    hooked = resize(img, n, 0.15, 0.85, seams, use_gpu=True, hook=True, transposed=transposed)
+    hooked = resize(img, n, 0.15, 0.85, seams, use_gpu=True, hook=True, transposed=transposed,
+                    verify=True)
     for r in (plain, hooked):
         assert r["status"] == dctenergy.DCTE_OK
         assert within_tol(r["emap"], O.energy_map(r["px"], n, 0.15, 0.85)).all()
     # without the hook the plug-in's counters stay untouched: served = the rest
     assert plain["fallback"] == plain["callbacks"] - plain["initial"] > 0
-    assert hooked["fallback"] == 0 and hooked["steps"] == seams
+    assert hooked["fallback"] == 0 and hooked["steps"] == seams and hooked["hook_on"] == 1
     assert hooked["served_map"] + hooked["served_band"] == hooked["callbacks"]
+    assert hooked["verified"] == hooked["served_band"] > 0 and hooked["bad"] == 0
     with dctenergy.Context(ngpus=1) as ctx:
         assert np.array_equal(hooked["emap"], ctx.energy_map(hooked["px"], n, 0.15, 0.85))
     print(n, transposed, "served without hook",
           (plain["callbacks"] - plain["fallback"]) / plain["callbacks"], "with hook", 1.0)
 
 
+def two_flat_stripes():
+    """natural frame with two flat vertical stripes of different grey: both
+    interiors have E = 0, so the DP's last row ties between them, and a
+    leftmost and a rightmost tie rule carve seams 40 columns apart"""
+    img = load_input("natural_rgb_97x41.npy").copy()
+    img[:, 14:30] = 60
+    img[:, 62:78] = 200
+    return img
+
+
 @pytest.mark.gpu
-def test_seam_hook_follows_liblqr_and_lets_go_on_divergence():
+def test_seam_hook_follows_liblqr():
     """The fake liblqr's seams are the ones the GPU search finds on the GPU
-    maps of the successively carved frames (the mirror carves the same
-    pixels); and when liblqr's image is not the frame the mirror carves
-    (perturbed after the build), the centre-pixel check switches the hook
-    off at the first update callback and the original code answers."""
+    maps of the successively carved frames: the mirror carves the same
+    pixels, and the hook stays on."""
     img = load_input("natural_rgb_97x41.npy")
-    r = resize(img, 8, 0.3, 0.7, 5, use_gpu=True, hook=True)
+    r = resize(img, 8, 0.3, 0.7, 5, use_gpu=True, hook=True, verify=True)
     with dctenergy.Context(ngpus=1) as ctx:
         px = np.ascontiguousarray(img)
         for k in range(5):
@@ -140,9 +171,35 @@ def test_seam_hook_follows_liblqr_and_lets_go_on_divergence():
             px = np.ascontiguousarray(np.stack([np.delete(px[y], s[y], axis=0)
                                                 for y in range(px.shape[0])]))
     assert np.array_equal(px, r["px"])
-    d = resize(img, 8, 0.3, 0.7, 5, use_gpu=True, hook=True, perturb=True)
-    assert d["steps"] == 1 and d["served_band"] == 0
-    assert d["fallback"] == d["callbacks"] - d["initial"] > 0
+    assert r["hook_on"] == 1 and r["bad"] == 0 and r["fallback"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [4, 8, 16])
+@pytest.mark.parametrize("diverge", ["perturb", "shift_row", "rightmost_ties"])
+def test_seam_hook_never_serves_a_foreign_window(n, diverge):
+    """liblqr departs from the mirror: its image is perturbed after the build,
+    or every seam it carves differs from the mirror's by one column in one
+    row, or its DP breaks ties to the right (two flat stripes tie the last
+    row 40 columns apart).  The hook checks each callback's whole reading
+    window against the mirror's pixels before it serves, so every value it
+    serves equals the original body's for that window (re-run on each: 0 off
+    tolerance), the first mismatch switches it off, and the original body
+    answers from there: liblqr's final energies are the reference map of its
+    carved image."""
+    img = two_flat_stripes() if diverge == "rightmost_ties" else load_input("natural_rgb_97x41.npy")
+    seams = 6
+    ref_seams = resize(img, n, 0.3, 0.7, seams, use_gpu=True, hook=True)["seams"]
+    d = resize(img, n, 0.3, 0.7, seams, use_gpu=True, hook=True, diverge=diverge, verify=True)
+    assert d["status"] == dctenergy.DCTE_OK
+    assert not np.array_equal(d["seams"], ref_seams), "the fake liblqr did not diverge"
+    assert d["bad"] == 0 and d["verified"] == d["served_band"]
+    assert d["hook_on"] == 0 and d["fallback"] > 0
+    assert d["served_map"] + d["served_band"] + d["fallback"] == d["callbacks"]
+    assert within_tol(d["emap"], O.energy_map(d["px"], n, 0.3, 0.7)).all()
+    if diverge == "perturb":
+        assert d["steps"] == 1 and d["served_band"] == 0
+    print(n, diverge, "served before the switch-off:", d["served_band"], "misses:", d["missed"])
 
 
 @pytest.mark.parametrize("n", [2, 4, 8, 16])
@@ -196,7 +253,7 @@ def test_carver_mirror_band_is_the_map_of_the_carved_frame(n, transposed):
         c, first = ctx.carver(img, n, 0.3, 0.7, transposed)
         assert np.array_equal(first, ctx.energy_map(px, n, 0.3, 0.7))
         H = px.shape[0]
-        assert c.height == H and c.width == px.shape[1] and c.band_width == 2 * n + 4
+        assert c.height == H and c.width == px.shape[1] and c.band_width == 4 * n + 4
         for _ in range(6):
             want = ctx.seam_find(ctx.energy_map(px, n, 0.3, 0.7))
             seam, x0, e, bpx = c.step()

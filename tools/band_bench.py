@@ -24,8 +24,6 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--tile-h", type=int, default=0)
     ap.add_argument("--lib", default=None, help="libdctenergy_hip.so to load (A/B)")
-    ap.add_argument("--wide", default="0,1",
-                    help="DCTE_OPT_WIDE_BANDS settings to compare, interleaved (e.g. 0,1)")
     ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
     if a.lib:
@@ -48,11 +46,9 @@ def main():
                                   n, 0.3, 0.7, out[y0 - Y0:].data_ptr(), out.stride(0), s.cuda_stream)
         pats = {"one launch": [(Y0, Y1)],
                 "interior + 2 edge launches (bench.py world > 1)": [(Y0 + hl, Y1 - hr), (Y0, Y0 + hl), (Y1 - hr, Y1)]}
-        wides = [int(v) for v in a.wide.split(",")]
         res = {}
         for rnd in range(a.rounds):
-            for wide in wides:
-                ctx.set_option(dctenergy.DCTE_OPT_WIDE_BANDS, wide)
+            for wide in (0,):
                 for name, ranges in pats.items():
                     for _ in range(5):
                         for r in ranges:

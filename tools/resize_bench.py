@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--seams", type=int, default=16)
     ap.add_argument("--n", type=int, default=8)
     ap.add_argument("--transposed", action="store_true")
+    ap.add_argument("--verify", action="store_true",
+                    help="re-run the original body on every hook-served callback (not timed fairly)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -32,7 +34,8 @@ def main():
     w, h = (int(v) for v in a.size.split("x"))
     img = synth.natural_rows(0, h, w, 3, seed=0, device="cuda").cpu().numpy()
     for hook in (False, True):
-        r = resize(img, a.n, 0.3, 0.7, a.seams, use_gpu=True, hook=hook, transposed=a.transposed)
+        r = resize(img, a.n, 0.3, 0.7, a.seams, use_gpu=True, hook=hook, transposed=a.transposed,
+                   verify=a.verify)
         upd = r["callbacks"] - r["initial"]
         print(json.dumps({
             "frame": f"{w}x{h} RGB", "n": a.n, "seams": a.seams, "transposed": a.transposed,
@@ -40,7 +43,8 @@ def main():
             "update_callbacks": upd, "update_callbacks_per_seam": round(upd / a.seams, 1),
             "served_gpu": r["callbacks"] - r["fallback"],
             "served_frac": round((r["callbacks"] - r["fallback"]) / r["callbacks"], 4),
-            "fallback": r["fallback"], "mirror_steps": r["steps"],
+            "fallback": r["fallback"], "mirror_steps": r["steps"], "hook_misses": r["missed"],
+            "hook_on_at_end": r["hook_on"], "verified": r["verified"], "verified_off_tol": r["bad"],
             "update_ms_per_seam": round(r["update_ns"] / 1e6 / a.seams, 3)}), flush=True)
 
 

@@ -26,8 +26,6 @@ def main():
     ap.add_argument("--width", type=int, default=16384)
     ap.add_argument("--tile-h", type=int, default=128)
     ap.add_argument("--n", type=int, default=8)
-    ap.add_argument("--wide", type=int, default=0,
-                    help="DCTE_OPT_WIDE_BANDS (1: 1024-thread lockstep tiles for short launches)")
     a = ap.parse_args()
     os.environ["DCTE_LIB"] = os.path.abspath(a.lib)
     import numpy as np
@@ -43,16 +41,11 @@ def main():
     s = torch.cuda.current_stream()
     tw = 256 if n != 16 else 64
     nwg = ((W + tw - 1) // tw) * ((R + a.tile_h - 1) // a.tile_h)
-    wide = bool(a.wide) and n == 8 and nwg <= 2 * 4 * 256   # the library's choice (dcte_capi.cpp)
-    if wide:
-        tw = 1024
-        nwg = ((W + tw - 1) // tw) * ((R + a.tile_h - 1) // a.tile_h)
-    slots = 1 if wide else 4                                # workgroups a CU holds at once
+    slots = 4                                               # workgroups a CU holds at once
     stamps = torch.zeros(3 * nwg, dtype=torch.int64, device="cuda")
     with dctenergy.Context(ngpus=1) as ctx:
         ctx.set_option(dctenergy.DCTE_OPT_TILE_H, a.tile_h)
         ctx.set_option(dctenergy.DCTE_OPT_TSTAMP_BUF, stamps.data_ptr())
-        ctx.set_option(dctenergy.DCTE_OPT_WIDE_BANDS, a.wide)
         ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, 0.0)     # the map launch alone
         for _ in range(6):
             ctx.energy_map_device(buf.data_ptr(), buf.stride(0), W, H, 3, Y0 - hl, buf.shape[0],
@@ -67,7 +60,7 @@ def main():
     dur = end - start
     cu = (hwid >> 8) & 15
     se = (hwid >> 13) & 7
-    res = {"rows": R, "tile_h": a.tile_h, "wide": wide, "workgroups": int(nwg),
+    res = {"rows": R, "tile_h": a.tile_h, "workgroups": int(nwg),
            "launch_span_us": us(end.max() - t0),
            "start_spread_us": us(start.max() - t0),
            "start_p50_us": us(np.percentile(start - t0, 50)),
