@@ -35,10 +35,13 @@ static void release_hook(dcte_map_cache *c)
     free(c->band_x0);
     free(c->band_e);
     free(c->band_px);
+    free(c->ver_lo);
+    free(c->ver_hi);
     c->mirror = NULL;
     c->band_x0 = NULL;
     c->band_e = NULL;
     c->band_px = NULL;
+    c->ver_lo = c->ver_hi = NULL;
     c->band_valid = c->hook_ok = 0;
 }
 
@@ -70,7 +73,9 @@ int dcte_plugin_build_ex(dcte_map_cache *c, const uint8_t *px, int w, int h, int
             c->band_x0 = (int *)malloc(sizeof(int) * (size_t)c->mh);
             c->band_e = (float *)malloc(sizeof(float) * (size_t)c->mh * c->bw);
             c->band_px = (unsigned char *)malloc((size_t)c->mh * c->bw * bpp);
-            c->hook_ok = c->band_x0 && c->band_e && c->band_px;
+            c->ver_lo = (int *)malloc(sizeof(int) * (size_t)c->mh);
+            c->ver_hi = (int *)malloc(sizeof(int) * (size_t)c->mh);
+            c->hook_ok = c->band_x0 && c->band_e && c->band_px && c->ver_lo && c->ver_hi;
             if (!c->hook_ok) release_hook(c);
         }
         if (!c->mirror && ho) {           /* no mirror: the map_t build below */
@@ -152,30 +157,55 @@ static double lqr_luma(const unsigned char *q, int bpp)
 
 static int clamp_int(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
 
-int dcte_plugin_window_check(const dcte_map_cache *c, int x, int y, int w, int h,
-                             double *const *data)
+/* compare liblqr's luma at columns [a, b] of row yy with the band; 1 / 0 / -1 */
+static int check_span(dcte_map_cache *c, int x, int y, int yy, int a, int b,
+                      dcte_rwindow_read_fn rd, void *rw)
 {
-    if (!c || !c->band_valid || !data || w != c->mw || h != c->mh) return 0;
+    const int k0 = a - c->band_x0[yy];
+    if (k0 < 0 || b - c->band_x0[yy] >= c->bw) return 0;
+    const unsigned char *q = c->band_px + ((size_t)yy * c->bw + (size_t)k0) * c->bpp;
+    for (int xx = a; xx <= b; xx++, q += c->bpp) {
+        c->reads++;
+        if (!(fabs(lqr_luma(q, c->bpp) - rd(rw, xx - x, yy - y)) <= 1e-9)) return -1;
+    }
+    return 1;
+}
+
+int dcte_plugin_window_check(dcte_map_cache *c, int x, int y, int w, int h,
+                             dcte_rwindow_read_fn rd, void *rw)
+{
+    if (!c || !c->band_valid || !rd || w != c->mw || h != c->mh) return 0;
     luma_tables();
     const int r = c->n / 2;
-    for (int i = -r + 1; i <= r; i++) {         /* the reference's gather order, render.c:146-152 */
-        const int xx = clamp_int(x + i, 0, w - 1);
-        const double *line = data[i + r - 1];
-        for (int j = -r + 1; j <= r; j++) {
-            const int yy = clamp_int(y + j, 0, h - 1);
-            const int k = xx - c->band_x0[yy];
-            if (k < 0 || k >= c->bw) return 0;
-            const double l = lqr_luma(c->band_px + ((size_t)yy * c->bw + (size_t)k) * c->bpp, c->bpp);
-            if (!(fabs(l - line[j + r - 1]) <= 1e-9)) return -1;
+    /* the window's columns: the clamped offsets of render.c:146-152 cover
+     * exactly [max(0, x - r + 1), min(w - 1, x + r)] (clamping repeats edge
+     * columns, it adds none); rows likewise */
+    const int a = clamp_int(x - r + 1, 0, w - 1), b = clamp_int(x + r, 0, w - 1);
+    const int y0 = clamp_int(y - r + 1, 0, h - 1), y1 = clamp_int(y + r, 0, h - 1);
+    for (int yy = y0; yy <= y1; yy++) {
+        int lo = c->ver_lo[yy], hi = c->ver_hi[yy], rc = 1;
+        if (a >= lo && b <= hi) continue;              /* checked by an earlier callback */
+        if (lo <= hi && a <= hi + 1 && b >= lo - 1) {  /* extend the checked interval */
+            if (a < lo) rc = check_span(c, x, y, yy, a, lo - 1, rd, rw);
+            if (rc == 1 && b > hi) rc = check_span(c, x, y, yy, hi + 1, b, rd, rw);
+            lo = a < lo ? a : lo;
+            hi = b > hi ? b : hi;
+        } else {                                       /* a new interval */
+            rc = check_span(c, x, y, yy, a, b, rd, rw);
+            lo = a;
+            hi = b;
         }
+        if (rc != 1) return rc;
+        c->ver_lo[yy] = lo;
+        c->ver_hi[yy] = hi;
     }
     return 1;
 }
 
 int dcte_plugin_lookup_hook(dcte_map_cache *c, int x, int y, int w, int h, int orientation,
-                            double *const *data, float *out)
+                            dcte_rwindow_read_fn rd, void *rw, float *out)
 {
-    if (!c || !c->valid || !c->hook_ok || !data || orientation != c->hook_orientation ||
+    if (!c || !c->valid || !c->hook_ok || !rd || orientation != c->hook_orientation ||
         h != c->mh || x < 0 || y < 0 || x >= w || y >= h)
         return 0;
     /* liblqr carved since the mirror's last step: carve as many seams */
@@ -188,14 +218,18 @@ int dcte_plugin_lookup_hook(dcte_map_cache *c, int x, int y, int w, int h, int o
         c->mw--;
         c->steps++;
         c->band_valid = 1;
+        for (int i = 0; i < c->mh; i++) {          /* nothing of the new band checked yet */
+            c->ver_lo[i] = 1;
+            c->ver_hi[i] = 0;
+        }
     }
-    const int k = x - (c->band_valid && w == c->mw ? c->band_x0[y] : 0);
-    const int chk = k >= 0 && k < c->bw ? dcte_plugin_window_check(c, x, y, w, h, data) : 0;
-    if (chk <= 0) {
+    const int chk = dcte_plugin_window_check(c, x, y, w, h, rd, rw);
+    const int k = chk == 1 ? x - c->band_x0[y] : -1;
+    if (chk <= 0 || k < 0 || k >= c->bw) {
         /* a window that differs from the mirror, or reaches past a band that
          * holds every window of liblqr's update region while the two carve the
          * same seams: the mirror no longer follows liblqr's image */
-        if (chk == 0) c->out_of_band++;
+        if (chk >= 0) c->out_of_band++;
         release_hook(c);
         c->missed++;
         return 0;

@@ -43,7 +43,8 @@ typedef struct {
     int *band_x0;          /* mh: first band column per row */
     float *band_e;         /* mh x bw energies of the last step's band */
     unsigned char *band_px;/* mh x bw x bpp pixels of the carved frame (window check) */
-    long long served_band, missed, out_of_band, steps;
+    int *ver_lo, *ver_hi;  /* mh: columns of each row already checked against liblqr this step */
+    long long served_band, missed, out_of_band, steps, reads;
 } dcte_map_cache;
 
 #define DCTE_PLUGIN_SEAM_HOOK 1u
@@ -72,30 +73,39 @@ int dcte_plugin_build_ex(dcte_map_cache *c, const uint8_t *px, int w, int h, int
 int dcte_plugin_lookup(const dcte_map_cache *c, int x, int y, int w, int h,
                        int orientation, float *out);
 
+/* What the hook reads liblqr's image through: the callback's reading window,
+ * rd(rw, dx, dy) = lqr_rwindow_read(rw, dx, dy, 0) (src/render.c:150), for
+ * offsets of the window the callback would gather (dx, dy in -(r - 1) .. r,
+ * r = n / 2, already clamped to the frame like clamp_offset_to_border,
+ * src/render.c:122-132). */
+typedef double (*dcte_rwindow_read_fn)(void *rw, int dx, int dy);
+
 /* The seam hook, for the callbacks dcte_plugin_lookup misses: when the
  * carver has become narrower than the mirror (liblqr carved a seam), the
  * mirror carves its own seam on the GPU and pixels of its update band are
- * served.  `data` is the window the callback's original body has just
- * gathered -- params->data, data[i + r - 1][j + r - 1] = lqr_rwindow_read of
- * the clamped offsets (i, j), i, j in [-(r - 1), r], r = n / 2
- * (src/render.c:141-152).  A value is served only when EVERY element of that
- * window equals liblqr's luma of the mirror's pixel at the same clamped
- * position (|difference| <= 1e-9: distinct 8-bit lumas differ by >= 7.8e-7),
- * so the served energy is the energy of exactly the window the original body
- * would transform, whatever seam liblqr picked.  A window that differs from
- * the mirror, or has a pixel outside the band (which holds every window of
- * liblqr's update region while the two carve the same seams), means the
- * mirror no longer follows liblqr's image: the hook misses and switches
- * itself off for this carver.  Misses return 0: the callback then runs its
- * original transform. */
+ * served.  A value is served only when EVERY element of the N x N window the
+ * original body would gather (src/render.c:141-152: data[i][j] = read of the
+ * clamped offsets (i, j), i, j in -(r - 1) .. r) equals liblqr's luma of the
+ * mirror's pixel at the same position (|difference| <= 1e-9: distinct 8-bit
+ * lumas differ by >= 7.8e-7), so the served energy is the energy of exactly
+ * the window the original body would transform, whatever seam liblqr picked.
+ * liblqr's image does not change between the callbacks of one update pass, so
+ * each band pixel is read through `rd` and compared once per seam (per row, the
+ * interval of columns already checked grows with the callbacks): about two
+ * reads per callback instead of N^2.  A window that differs from the mirror,
+ * or has a pixel outside the band (which holds every window of liblqr's update
+ * region while the two carve the same seams), means the mirror no longer
+ * follows liblqr's image: the hook misses and switches itself off for this
+ * carver.  Misses return 0: the callback then runs its original body. */
 int dcte_plugin_lookup_hook(dcte_map_cache *c, int x, int y, int w, int h, int orientation,
-                            double *const *data, float *out);
+                            dcte_rwindow_read_fn rd, void *rw, float *out);
 
-/* The window test of dcte_plugin_lookup_hook alone, on the current band: 1 =
- * every element matches the mirror, 0 = a window pixel lies outside the band
- * (or no band), -1 = an element differs.  Exposed for tests. */
-int dcte_plugin_window_check(const dcte_map_cache *c, int x, int y, int w, int h,
-                             double *const *data);
+/* The window test of dcte_plugin_lookup_hook alone, on the current band (it
+ * records what it checked): 1 = every element matches the mirror, 0 = a
+ * window pixel lies outside the band (or no band), -1 = an element differs.
+ * Exposed for tests. */
+int dcte_plugin_window_check(dcte_map_cache *c, int x, int y, int w, int h,
+                             dcte_rwindow_read_fn rd, void *rw);
 
 void dcte_plugin_release(dcte_map_cache *c);
 

@@ -90,6 +90,13 @@ static float original_dct_pixel_energy(int x, int y, int w, int h, LqrReadingWin
     return window_energy(p);
 }
 
+/* the patch's adapter: the hook reads liblqr's image
+ * through the callback's reading window */
+static double rwindow_read(void *rw, int dx, int dy)
+{
+    return lqr_rwindow_read((LqrReadingWindow *)rw, dx, dy, 0);
+}
+
 static int g_orientation; /* lqr_carver_get_orientation of the fake carver */
 static int g_use_hook;    /* the plug-in was built with DCTE_PLUGIN_SEAM_HOOK */
 
@@ -102,18 +109,16 @@ static float dct_pixel_energy(int x, int y, int w, int h, LqrReadingWindow *rw, 
         g_served_map++;
         return v;
     }
-    if (!g_use_hook) return original_dct_pixel_energy(x, y, w, h, rw, extra);
-    gather_window(x, y, w, h, rw, p);
-    if (dcte_plugin_lookup_hook(&p->gpu, x, y, w, h, g_orientation, p->rows, &v)) {
+    if (g_use_hook && dcte_plugin_lookup_hook(&p->gpu, x, y, w, h, g_orientation, rwindow_read, rw, &v)) {
         if (g_verify) {  /* test mode: what the original body returns for this window */
+            gather_window(x, y, w, h, rw, p);
             const float ref = window_energy(p);
             g_verified++;
             if (!(fabsf(v - ref) <= 1e-5f * fabsf(ref) + 1e-9f)) g_bad++;
         }
         return v;
     }
-    g_fallback_calls++;
-    return window_energy(p);
+    return original_dct_pixel_energy(x, y, w, h, rw, extra);
 }
 
 /* Carver built on px (w x h, bpp), energy function registered with radius
@@ -224,17 +229,54 @@ static void seam_shift_one_row(int *s, int w, int h)
 }
 
 /* Self-test of the hook's window check on the host (no device): a synthetic
- * cache over a random w x h luma frame with a band around a fixed seam.
- * Returns 0 when (1) every window of the band's update pixels matches, (2) a
- * window with any one element off by one 8-bit luma step is rejected (-1) and
- * (3) windows reaching past the band miss (0); else the failing case's code. */
+ * cache over a random w x h luma frame with a band around a fixed seam, the
+ * update pixels visited in liblqr's order (rows outer, columns inner).
+ * Returns 0 when (1) every window matches, with fewer than 3 reads per
+ * callback on average (each pixel read once); (2) with any one pixel of the
+ * region moved by one 8-bit luma step, the first window holding it -- and no
+ * earlier one -- is rejected (-1); (3) a window past the band misses (0);
+ * else the failing case's code. */
+typedef struct {
+    int w, h, n, bpp, bw;
+    int *x0, *a, *b;        /* band start per row; update columns [a, b] per row */
+    unsigned char *bpx;
+    double *luma;
+} SelfTest;
+
+static void selftest_reset(dcte_map_cache *c, const SelfTest *t, int *lo, int *hi)
+{
+    memset(c, 0, sizeof(*c));
+    c->n = t->n;
+    c->mw = t->w;
+    c->mh = t->h;
+    c->bpp = t->bpp;
+    c->bw = t->bw;
+    c->band_valid = 1;
+    c->band_x0 = t->x0;
+    c->band_px = t->bpx;
+    for (int y = 0; y < t->h; y++) {
+        lo[y] = 1;
+        hi[y] = 0;
+    }
+    c->ver_lo = lo;
+    c->ver_hi = hi;
+}
+
 int fake_window_check_selftest(int n, int bpp, unsigned seed)
 {
-    const int w = 61, h = 23, r = n / 2, bw = 8 * r + 4;
+    SelfTest t;
+    t.w = 61;
+    t.h = 23;
+    t.n = n;
+    t.bpp = bpp;
+    const int w = t.w, h = t.h, r = n / 2, bw = t.bw = 8 * r + 4;
     unsigned char *px = (unsigned char *)malloc((size_t)w * h * bpp);
-    double *luma = (double *)malloc(sizeof(double) * (size_t)w * h);
-    int *x0 = (int *)malloc(sizeof(int) * h);
-    unsigned char *bpx = (unsigned char *)malloc((size_t)h * bw * bpp);
+    t.luma = (double *)malloc(sizeof(double) * (size_t)w * h);
+    t.x0 = (int *)malloc(sizeof(int) * h);
+    t.a = (int *)malloc(sizeof(int) * h);
+    t.b = (int *)malloc(sizeof(int) * h);
+    t.bpx = (unsigned char *)malloc((size_t)h * bw * bpp);
+    int *lo = (int *)malloc(sizeof(int) * h), *hi = (int *)malloc(sizeof(int) * h);
     int rc = 0;
     for (size_t i = 0; i < (size_t)w * h * bpp; i++) {
         seed = seed * 1664525u + 1013904223u;
@@ -243,74 +285,90 @@ int fake_window_check_selftest(int n, int bpp, unsigned seed)
     for (int y = 0; y < h; y++)
         for (int x = 0; x < w; x++) {
             const unsigned char *q = px + ((size_t)y * w + x) * bpp;
-            luma[(size_t)y * w + x] = bpp == 1 ? (double)q[0] / 255
+            t.luma[(size_t)y * w + x] = bpp == 1 ? (double)q[0] / 255
                 : 0.2126 * ((double)q[0] / 255) + 0.7152 * ((double)q[1] / 255) + 0.0722 * ((double)q[2] / 255);
         }
-    /* a seam wandering around column 30; band rows as dcte_band_gather builds them */
+    /* a seam wandering around column 30; band rows as dcte_band_gather builds
+     * them, update columns as fake_resize's update_emap */
     int s[23];
     for (int y = 0; y < h; y++) s[y] = 30 + (y % 5 < 3 ? y % 5 : 5 - y % 5);
     for (int y = 0; y < h; y++) {
-        int lo = w;
+        int m = w;
         for (int j = -2 * r; j <= 2 * r; j++) {
             const int yy = y + j < 0 ? 0 : y + j >= h ? h - 1 : y + j;
-            if (s[yy] < lo) lo = s[yy];
+            if (s[yy] < m) m = s[yy];
         }
-        int a = lo - 2 * r - 1, mx = w - bw > 0 ? w - bw : 0;
-        x0[y] = a < 0 ? 0 : a > mx ? mx : a;
+        int a = m - 2 * r - 1, mx = w - bw > 0 ? w - bw : 0;
+        t.x0[y] = a < 0 ? 0 : a > mx ? mx : a;
         for (int k = 0; k < bw; k++) {
-            const int x = x0[y] + k < w - 1 ? x0[y] + k : w - 1;
-            memcpy(bpx + ((size_t)y * bw + k) * bpp, px + ((size_t)y * w + x) * bpp, bpp);
+            const int x = t.x0[y] + k < w - 1 ? t.x0[y] + k : w - 1;
+            memcpy(t.bpx + ((size_t)y * bw + k) * bpp, px + ((size_t)y * w + x) * bpp, bpp);
         }
-    }
-    dcte_map_cache c;
-    memset(&c, 0, sizeof(c));
-    c.n = n;
-    c.mw = w;
-    c.mh = h;
-    c.bpp = bpp;
-    c.bw = bw;
-    c.band_valid = 1;
-    c.band_x0 = x0;
-    c.band_px = bpx;
-    EnergyParameters p;
-    params_init(&p, 0.3f, 0.7f, n);
-    LqrReadingWindow rw = {luma, w, h, 0, 0, r};
-    long long checked = 0;
-    for (int y = 0; y < h && !rc; y++) {
-        int a = w, b = -1;  /* update columns of row y (fake_resize's rule) */
+        t.a[y] = w;
+        t.b[y] = -1;
         for (int y1 = y - r; y1 <= y + r; y1++) {
             if (y1 < 0 || y1 >= h) continue;
-            if (s[y1] - r < a) a = s[y1] - r;
-            if (s[y1] + r - 1 > b) b = s[y1] + r - 1;
+            if (s[y1] - r < t.a[y]) t.a[y] = s[y1] - r;
+            if (s[y1] + r - 1 > t.b[y]) t.b[y] = s[y1] + r - 1;
         }
-        if (a < 0) a = 0;
-        if (b > w - 1) b = w - 1;
-        for (int x = a; x <= b && !rc; x++) {
+        if (t.a[y] < 0) t.a[y] = 0;
+        if (t.b[y] > w - 1) t.b[y] = w - 1;
+    }
+    dcte_map_cache c;
+    LqrReadingWindow rw = {t.luma, w, h, 0, 0, r};
+    /* (1) */
+    selftest_reset(&c, &t, lo, hi);
+    long long calls = 0;
+    for (int y = 0; y < h && !rc; y++)
+        for (int x = t.a[y]; x <= t.b[y] && !rc; x++) {
             rw.x = x;
             rw.y = y;
-            gather_window(x, y, w, h, &rw, &p);
-            if (dcte_plugin_window_check(&c, x, y, w, h, p.rows) != 1) rc = 1;
-            for (int e = 0; e < n * n && !rc; e += 7) {   /* one element off by one luma step */
-                const double keep = p.d[e];
-                p.d[e] = keep + (bpp == 1 ? 1.0 / 255 : 0.0722 / 255);
-                if (dcte_plugin_window_check(&c, x, y, w, h, p.rows) != -1) rc = 2;
-                p.d[e] = keep;
-            }
-            checked++;
+            if (dcte_plugin_window_check(&c, x, y, w, h, rwindow_read, &rw) != 1) rc = 1;
+            calls++;
         }
-    }
-    /* a pixel far left of the band: its window leaves it */
-    if (!rc) {
+    if (!rc && (calls == 0 || c.reads > 3 * calls)) rc = 4;
+    /* (2): every 5th pixel of the update windows' union */
+    for (int py = 0; py < h && !rc; py++)
+        for (int px0 = 0; px0 < w && !rc; px0 += 5) {
+            int first_y = -1, first_x = -1;   /* the first callback whose window holds it */
+            for (int y = 0; y < h && first_y < 0; y++)
+                for (int x = t.a[y]; x <= t.b[y]; x++)
+                    if (px0 >= x - r + 1 && px0 <= x + r && py >= y - r + 1 && py <= y + r) {
+                        first_y = y;
+                        first_x = x;
+                        break;
+                    }
+            if (first_y < 0) continue;
+            const double keep = t.luma[(size_t)py * w + px0];
+            t.luma[(size_t)py * w + px0] = keep + (bpp == 1 ? 1.0 / 255 : 0.0722 / 255);
+            selftest_reset(&c, &t, lo, hi);
+            int got = 1, at_y = -1, at_x = -1;
+            for (int y = 0; y < h && got == 1; y++)
+                for (int x = t.a[y]; x <= t.b[y] && got == 1; x++) {
+                    rw.x = x;
+                    rw.y = y;
+                    got = dcte_plugin_window_check(&c, x, y, w, h, rwindow_read, &rw);
+                    at_y = y;
+                    at_x = x;
+                }
+            if (got != -1 || at_y != first_y || at_x != first_x) rc = 2;
+            t.luma[(size_t)py * w + px0] = keep;
+        }
+    /* (3) a pixel far left of the band: its window leaves it */
+    if (!rc && t.x0[h / 2] > 0) {
+        selftest_reset(&c, &t, lo, hi);
         rw.x = 0;
         rw.y = h / 2;
-        gather_window(0, h / 2, w, h, &rw, &p);
-        if (x0[h / 2] > 0 && dcte_plugin_window_check(&c, 0, h / 2, w, h, p.rows) != 0) rc = 3;
+        if (dcte_plugin_window_check(&c, 0, h / 2, w, h, rwindow_read, &rw) != 0) rc = 3;
     }
-    if (!rc && checked == 0) rc = 4;
     free(px);
-    free(luma);
-    free(x0);
-    free(bpx);
+    free(t.luma);
+    free(t.x0);
+    free(t.a);
+    free(t.b);
+    free(t.bpx);
+    free(lo);
+    free(hi);
     return rc;
 }
 
@@ -327,11 +385,11 @@ int fake_window_check_selftest(int n, int bpp, unsigned seed)
  * The plug-in is built on px as in init_carver_from_vals; `hook` selects the
  * patched callback with the seam hook (DCTE_PLUGIN_SEAM_HOOK).  Outputs: the
  * final energies (fh x cw), the final image bytes (fh x cw x bpp), the seams
- * (seams x fh) and counts[10] = {callbacks, fallback (original transform),
+ * (seams x fh) and counts[11] = {callbacks, fallback (original transform),
  * served from a map, served from a seam band, mirror steps, nanoseconds spent
  * in the update_emap callbacks (incl. the mirror's steps), hook-served values
  * re-checked against the original body (verify), of those off tolerance,
- * hook misses, hook still on at the end}.
+ * hook misses, hook still on at the end, window reads of the hook's check}.
  * transposed: vertical resize -- the carver works on the transposed frame.
  * diverge (tests of the hook's window check): 0 = liblqr follows the
  * mirror's rules; 1 = after the build liblqr's image differs slightly from
@@ -434,6 +492,7 @@ int fake_resize(const uint8_t *px, int w, int h, int bpp, int n, float edges, fl
     counts[7] = g_bad;
     counts[8] = p.gpu.missed;
     counts[9] = p.gpu.hook_ok;
+    counts[10] = p.gpu.reads;
     dcte_plugin_release(&p.gpu);
     g_use_hook = g_verify = 0;
     free(img);

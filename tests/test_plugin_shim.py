@@ -77,7 +77,7 @@ def resize(img, n, e, t, seams, use_gpu, hook, transposed=False, diverge="none",
     emap = np.empty((fh, fw - seams), np.float32)
     px = np.empty((fh, fw - seams) + img.shape[2:], np.uint8)
     seam_cols = np.empty((max(seams, 1), fh), np.int32)
-    counts = (ctypes.c_longlong * 10)()
+    counts = (ctypes.c_longlong * 11)()
     status = ctypes.c_int()
     rc = fake().fake_resize(img.ctypes.data, w, h, bpp, n, e, t, int(use_gpu), int(hook), seams,
                             int(transposed), DIVERGE[diverge], int(verify), emap.ctypes.data,
@@ -86,7 +86,7 @@ def resize(img, n, e, t, seams, use_gpu, hook, transposed=False, diverge="none",
     c = list(counts)
     return {"emap": emap, "px": px, "seams": seam_cols[:seams], "callbacks": c[0],
             "fallback": c[1], "served_map": c[2], "served_band": c[3], "steps": c[4], "update_ns": c[5],
-            "verified": c[6], "bad": c[7], "missed": c[8], "hook_on": c[9],
+            "verified": c[6], "bad": c[7], "missed": c[8], "hook_on": c[9], "reads": c[10],
             "status": status.value, "initial": fw * fh}
 
 
@@ -140,6 +140,8 @@ def test_seam_hook_serves_update_emap(n, transposed):
     assert hooked["fallback"] == 0 and hooked["steps"] == seams and hooked["hook_on"] == 1
     assert hooked["served_map"] + hooked["served_band"] == hooked["callbacks"]
     assert hooked["verified"] == hooked["served_band"] > 0 and hooked["bad"] == 0
+    # each band pixel read once per seam: about two reads per update callback
+    assert hooked["reads"] < 4 * (hooked["callbacks"] - hooked["initial"])
     with dctenergy.Context(ngpus=1) as ctx:
         assert np.array_equal(hooked["emap"], ctx.energy_map(hooked["px"], n, 0.15, 0.85))
     print(n, transposed, "served without hook",
@@ -192,7 +194,8 @@ def test_seam_hook_never_serves_a_foreign_window(n, diverge):
     ref_seams = resize(img, n, 0.3, 0.7, seams, use_gpu=True, hook=True)["seams"]
     d = resize(img, n, 0.3, 0.7, seams, use_gpu=True, hook=True, diverge=diverge, verify=True)
     assert d["status"] == dctenergy.DCTE_OK
-    assert not np.array_equal(d["seams"], ref_seams), "the fake liblqr did not diverge"
+    if diverge != "perturb":   # (perturb: the same seams over a different image)
+        assert not np.array_equal(d["seams"], ref_seams), "the fake liblqr did not diverge"
     assert d["bad"] == 0 and d["verified"] == d["served_band"]
     assert d["hook_on"] == 0 and d["fallback"] > 0
     assert d["served_map"] + d["served_band"] + d["fallback"] == d["callbacks"]

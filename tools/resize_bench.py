@@ -45,6 +45,7 @@ def main():
             "served_frac": round((r["callbacks"] - r["fallback"]) / r["callbacks"], 4),
             "fallback": r["fallback"], "mirror_steps": r["steps"], "hook_misses": r["missed"],
             "hook_on_at_end": r["hook_on"], "verified": r["verified"], "verified_off_tol": r["bad"],
+            "hook_reads_per_update_callback": round(r["reads"] / max(upd, 1), 2),
             "update_ms_per_seam": round(r["update_ns"] / 1e6 / a.seams, 3)}), flush=True)
 
 
