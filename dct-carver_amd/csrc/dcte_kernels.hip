@@ -75,8 +75,10 @@ constexpr unsigned kBufFlags = 0x00020000u;  // gfx9 raw buffer dword3
 #ifndef DCTE_FIX_DIRECT8
 #define DCTE_FIX_DIRECT8 16u    // N = 8: most flagged pixels a strip may hold and still be sparse (128 before: dots +47 %, text +4 %; profiles/r03/fix_direct_ab.jsonl)
 #endif
+// (N = 2, 4 keep r02's 128: their dense strips take the band path of
+// dcte_fix_strips, which that value was tuned for, profiles/r02/fix_direct.jsonl)
 template <int N>
-constexpr unsigned kFixDirect = N == 16 ? 32u : (unsigned)DCTE_FIX_DIRECT8;
+constexpr unsigned kFixDirect = N == 16 ? 32u : (N == 8 ? (unsigned)DCTE_FIX_DIRECT8 : 128u);
 // dense strips walked by a lane-per-pixel (N = 8, fix_dense8_run) /
 // lane-quad-per-pixel (N = 16 liblqr, fix_dense16_flat) walk rather than the
 // band path of dcte_fix_strips
