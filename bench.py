@@ -402,6 +402,18 @@ def main():
                               n, e, t, out[y0 - band.Y0:].data_ptr(), out.stride(0), st,
                               dev_index)
 
+    def run_edges(st=stream):
+        """the band's halo-dependent rows: both edge ranges in ONE map launch
+        and one refinement launch (dcte_energy_map_device2)"""
+        eds = band.edges()
+        if len(eds) == 2:
+            (a0, a1), (b0, b1) = eds
+            ctx.energy_map_device2(buf.data_ptr(), buf.stride(0), W, H, 3, row0, band.rows, a0, a1,
+                                   b0, b1, n, e, t, out[a0 - band.Y0:].data_ptr(), out.stride(0), st,
+                                   dev_index)
+        for a, b in (eds if len(eds) == 1 else []):
+            run_rows(a, b, st)
+
     # halo-dependent edge rows on a stream of their own: they wait for the
     # halos only, so they run beside the interior instead of after it
     # (tools/band_split.py: 8 -> 2 us of split overhead per 2048-row band)
@@ -423,21 +435,18 @@ def main():
                 buf[:band.top].copy_(host_buf[:band.top], non_blocking=True)
             if band.bot:
                 buf[band.rows - band.bot:].copy_(host_buf[band.rows - band.bot:], non_blocking=True)
-            for a, b in band.edges():
-                run_rows(a, b)
+            run_edges()
         elif edge_stream is not None:
             reqs = D.exchange_halos(buf, band)   # after this rank's previous step (incl. its edges)
             run_rows(i0, i1)                     # overlaps the exchange
             with torch.cuda.stream(edge_stream):
                 for r in reqs:
                     r.wait()                     # the edge stream waits for the halos
-                for a, b in band.edges():
-                    run_rows(a, b, edge_stream.cuda_stream)
+                run_edges(edge_stream.cuda_stream)
             torch.cuda.current_stream(dev).wait_stream(edge_stream)
         else:
             run_rows(i0, i1)
-            for a, b in band.edges():
-                run_rows(a, b)
+            run_edges()
 
     for _ in range(args.warmup):
         step()

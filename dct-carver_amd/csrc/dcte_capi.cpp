@@ -259,28 +259,40 @@ dcte::FixParams fix_params(const uint8_t* px, long long rowstride, int w, int h,
 
 int ensure_buf(dcte_ctx* ctx, void** p, size_t* cap, size_t bytes);
 
+// Output rows [y0, y1) -- plus [yb0, yb1) when yb0 < yb1 (y1 <= yb0: one
+// launch for both, the out row of y at d_out + (y - y0) * out_stride).
 int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, int w, int h,
                int bpp, int in_row0, int in_rows, int y0, int y1, int n, float edges,
-               float textures, int sem, float* d_out, long long out_stride, hipStream_t s)
+               float textures, int sem, float* d_out, long long out_stride, hipStream_t s,
+               int yb0 = 0, int yb1 = 0)
 {
     DCTE_ARG(ctx, valid_n(n) && valid_sem_bpp(sem, bpp) && w > 0 && h > 0);
     DCTE_ARG(ctx, y0 >= 0 && y1 <= h && y0 <= y1 && d_px && d_out && out_stride >= w);
     DCTE_ARG(ctx, rowstride >= (long long)w * bpp);
-    if (y1 == y0) return DCTE_OK;
-    int lo, hi;
-    needed_rows(n, sem, h, y0, y1, lo, hi);
+    const bool two = yb0 < yb1;
+    DCTE_ARG(ctx, !two || (yb0 >= y1 && yb1 <= h));
+    if (!two) yb0 = yb1 = y1;
+    if (y1 == y0 && !two) return DCTE_OK;
+    int lo, hi, lo2, hi2;
+    needed_rows(n, sem, h, y1 > y0 ? y0 : yb0, two ? yb1 : y1, lo, hi);
     DCTE_ARG(ctx, lo >= in_row0 && hi < in_row0 + in_rows);
+    if (two && y1 > y0) {                    // both ranges' rows must be readable
+        needed_rows(n, sem, h, y0, y1, lo2, hi2);
+        DCTE_ARG(ctx, lo2 >= in_row0 && hi2 < in_row0 + in_rows);
+    }
     // one buffer resource addresses the readable rows: < 4 GiB
     long long span = (long long)(in_rows - 1) * rowstride + (long long)w * bpp + 3;
     if (span >= (1LL << 32)) return DCTE_ERANGE;
-    size_t npix = (size_t)(y1 - y0) * (size_t)w;
+    size_t npix = (size_t)((two ? yb1 : y1) - y0) * (size_t)w;
     if (npix >= (1ULL << 32)) return DCTE_ERANGE;
     // one workgroup's output rows go through one buffer resource; a band
     // shorter than a tile is one tile of exactly its rows (same results, and
     // the refinement list below is sized for the rows that exist)
+    const int rows_a = y1 - y0, rows_b = yb1 - yb0;
     int tile_h = ctx->tile_h > 0 ? ctx->tile_h : dcte::map_default_tile_h(n);
-    if (tile_h > y1 - y0) tile_h = y1 - y0;
+    if (tile_h > (rows_a > rows_b ? rows_a : rows_b)) tile_h = rows_a > rows_b ? rows_a : rows_b;
     if ((long long)tile_h * out_stride * 4 >= (1LL << 31)) return DCTE_ERANGE;
+    const int tiles_a = dcte::map_tiles_y(n, rows_a, tile_h);
 
     DCTE_HIP(ctx, hipSetDevice(d.id));
     // N = 8 launches of at most two rounds of workgroups (a strong-scaling
@@ -295,11 +307,12 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
         if (d.cus <= 0 &&
             hipDeviceGetAttribute(&d.cus, hipDeviceAttributeMultiprocessorCount, d.id) != hipSuccess)
             d.cus = 256;
-        const long long nwg = (long long)dcte::map_tiles_x(n, w) * dcte::map_tiles_y(n, y1 - y0, tile_h);
+        const long long nwg = (long long)dcte::map_tiles_x(n, w) *
+                              (tiles_a + dcte::map_tiles_y(n, rows_b, tile_h));
         if (nwg <= 2LL * 4 * d.cus) fair = 3;
     }
     // refinement lists: one region of 64 * tile_h entries per 64-column strip
-    const int tiles_x = dcte::map_tiles_x(n, w), tiles_y = dcte::map_tiles_y(n, y1 - y0, tile_h);
+    const int tiles_x = dcte::map_tiles_x(n, w), tiles_y = tiles_a + dcte::map_tiles_y(n, rows_b, tile_h);
     if (tiles_y > kMaxGridY) {
         ctx->last_error = "tile rows exceed the launch grid (raise DCTE_OPT_TILE_H)";
         return DCTE_ERANGE;
@@ -329,7 +342,11 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     p.in_rows = in_rows;
     p.y0 = y0;
     p.y1 = y1;
+    p.yb0 = yb0;
+    p.yb1 = yb1;
     p.tile_h = tile_h;
+    p.tiles_a = tiles_a;
+    p.tiles_y = tiles_y;
     p.fair = fair;
     p.out = d_out;
     p.out_stride = out_stride;
@@ -692,6 +709,19 @@ int dcte_energy_map_device(dcte_ctx* ctx, int device, const void* d_px, long lon
     if (!ctx || device < 0 || device >= (int)ctx->devs.size()) return DCTE_EINVAL;
     return run_device(ctx, ctx->devs[device], d_px, rowstride, w, h, bpp, in_row0, in_rows, y0,
                       y1, n, edges, textures, semantics, d_out, out_stride, (hipStream_t)stream);
+}
+
+int dcte_energy_map_device2(dcte_ctx* ctx, int device, const void* d_px, long long rowstride,
+                            int w, int h, int bpp, int in_row0, int in_rows, int y0, int y1,
+                            int yb0, int yb1, int n, float edges, float textures, int semantics,
+                            float* d_out, long long out_stride, void* stream)
+{
+    DeviceGuard guard_;
+    if (!ctx || device < 0 || device >= (int)ctx->devs.size()) return DCTE_EINVAL;
+    DCTE_ARG(ctx, yb0 <= yb1);
+    return run_device(ctx, ctx->devs[device], d_px, rowstride, w, h, bpp, in_row0, in_rows, y0,
+                      y1, n, edges, textures, semantics, d_out, out_stride, (hipStream_t)stream,
+                      yb0, yb1);
 }
 
 int dcte_seam_carve_device(dcte_ctx* ctx, int device, const void* d_px, long long rowstride, int w,

@@ -8,18 +8,24 @@
 
 namespace dcte {
 
-// One launch computes output rows [y0, y1) of a w x h image.  The input
-// pointer addresses global row `in_row0`; rows [in_row0, in_row0 + in_rows)
-// are readable.  Every row the window clamp can touch for [y0, y1)
-// (clamp(y0 - N/2 + 1) .. clamp(y1 - 1 + N/2)) must be readable: a row band
-// plus its halo, or the whole frame.
+// One launch computes output rows [y0, y1) of a w x h image -- and, when
+// yb0 < yb1, rows [yb0, yb1) too (y1 <= yb0): a strong-scaling rank's two
+// halo-dependent edge ranges in ONE launch.  Tile rows 0 .. tiles_a - 1 cover
+// the first range, the rest the second (tile_row0 / tile_row1 below), so no
+// workgroup straddles the gap.  The input pointer addresses global row
+// `in_row0`; rows [in_row0, in_row0 + in_rows) are readable.  Every row the
+// window clamp can touch for the output rows (clamp(y0 - N/2 + 1) ..
+// clamp(last - 1 + N/2)) must be readable: a row band plus its halo, or the
+// whole frame.
 struct MapParams {
     const uint8_t* px;
     long long rowstride;     // bytes
     int w, h;                // global image size
     int in_row0, in_rows;    // readable input rows (global)
     int y0, y1;              // output rows (global)
+    int yb0, yb1;            // second output range (global; empty: yb0 = yb1)
     int tile_h;              // output rows per workgroup
+    int tiles_a, tiles_y;    // tile rows of [y0, y1); of the launch
     int fair;                // > 0: priority levels a workgroup steps down through its tile
     float* out;              // row y at out + (y - y0) * out_stride
     long long out_stride;    // floats
@@ -56,6 +62,17 @@ struct MapParams {
     // end, HW_ID}, a buffer nothing else reads (null: no stamps)
     unsigned long long* stamps;
 };
+
+// first / one-past-last output row of the launch's tile row `by`
+__host__ __device__ inline int tile_row0(const MapParams& p, int by)
+{
+    return by < p.tiles_a ? p.y0 + by * p.tile_h : p.yb0 + (by - p.tiles_a) * p.tile_h;
+}
+__host__ __device__ inline int tile_row1(const MapParams& p, int by)
+{
+    const int r = tile_row0(p, by) + p.tile_h, e = by < p.tiles_a ? p.y1 : p.yb1;
+    return r < e ? r : e;
+}
 
 // dcte_fix_strips: the map launch's own parameters plus the fp64 pieces
 struct TileFixParams {

@@ -182,8 +182,8 @@ __global__ __launch_bounds__((Geo<N, SEM>::T), MapThreads<N>::min_waves) void dc
     }
     const int x0 = bx * TW;
     const int x = x0 + c;
-    const int ys = p.y0 + by * p.tile_h;
-    const int ye = min(ys + p.tile_h, p.y1);
+    const int ys = tile_row0(p, by);
+    const int ye = tile_row1(p, by);
     const int n_in = (ye - ys) + N - 1;
     const int ngroups = (n_in + G - 1) / G;
     const int w = p.w, h = p.h;
@@ -956,7 +956,7 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
         const unsigned tile = strip / spt;
         const int bx = (int)(tile % (unsigned)tp.tiles_x), by = (int)(tile / (unsigned)tp.tiles_x);
         const int sx0 = bx * tp.tile_w + 64 * (int)(strip % spt);
-        const int ys = p.y0 + by * p.tile_h;
+        const int ys = tile_row0(p, by);
         const unsigned* list = p.fix_list + (size_t)strip * (size_t)(64 * p.tile_h);
         for (unsigned q0 = 0; q0 < cnt; q0 += 64) {   // uniform
             const unsigned q = q0 + (unsigned)lane;
@@ -1054,8 +1054,7 @@ struct DenseWalk {
         per_strip = 64u * (unsigned)p.tile_h;
         // the map launch numbered at most this many strips (a counter that did
         // not start at zero must not send the walk past the lists)
-        const unsigned nstrips = (unsigned)t.tiles_x * ((unsigned)t.tile_w / 64u) *
-                                 (unsigned)((p.y1 - p.y0 + p.tile_h - 1) / p.tile_h);
+        const unsigned nstrips = (unsigned)t.tiles_x * ((unsigned)t.tile_w / 64u) * (unsigned)p.tiles_y;
         if (nd > nstrips || total > nstrips * per_strip) return false;   // uniform
         nb = (total + EPB - 1) / EPB;
         // chunks of up to DCTE_DENSE_CHUNK consecutive batches while every
@@ -1108,12 +1107,12 @@ __global__ __launch_bounds__(256) void dcte_dense_index(const TileFixParams tp)
     const unsigned slot = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
     const unsigned nd = (unsigned)(*p.dense_ctr >> 32);
     const unsigned spt = (unsigned)tp.tile_w / 64u;
-    const unsigned nstrips = (unsigned)tp.tiles_x * spt * (unsigned)((p.y1 - p.y0 + p.tile_h - 1) / p.tile_h);
+    const unsigned nstrips = (unsigned)tp.tiles_x * spt * (unsigned)p.tiles_y;
     if (slot >= nd || nd > nstrips) return;            // uniform per wave
     const uint2 v = p.dense_list[slot];
     const unsigned strip = v.x, off = v.y, cnt = p.tile_count[strip], tile = strip / spt;
     const uint4 di = make_uint4((unsigned)((int)(tile % (unsigned)tp.tiles_x) * tp.tile_w + 64 * (int)(strip % spt)),
-                                (unsigned)(p.y0 + (int)(tile / (unsigned)tp.tiles_x) * p.tile_h), strip, off);
+                                (unsigned)tile_row0(p, (int)(tile / (unsigned)tp.tiles_x)), strip, off);
     const unsigned first = (off + EPB - 1u) / EPB, last = (off + cnt - 1u) / EPB;
     for (unsigned b = first + lane; b <= last; b += 64u) p.dense_batch[b] = di;
 }
@@ -1475,8 +1474,8 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
         const unsigned tile = strip / SPT;
         const int bx = (int)(tile % (unsigned)tp.tiles_x), by = (int)(tile / (unsigned)tp.tiles_x);
         g.sx0 = bx * TW + 64 * (int)(strip % SPT);
-        g.ys = p.y0 + by * p.tile_h;
-        g.ye = min(g.ys + p.tile_h, p.y1);
+        g.ys = tile_row0(p, by);
+        g.ye = tile_row1(p, by);
         g.list = p.fix_list + (size_t)strip * (size_t)(64 * p.tile_h);
         return g;
     };
@@ -1931,7 +1930,7 @@ template <int N, int BPP, int SEM>
 static hipError_t launch_map_t(const MapParams& p, hipStream_t s)
 {
     constexpr int TW = Geo<N, SEM>::TW;
-    dim3 grid((p.w + TW - 1) / TW, (p.y1 - p.y0 + p.tile_h - 1) / p.tile_h);
+    dim3 grid((p.w + TW - 1) / TW, p.tiles_y);
     hipLaunchKernelGGL((dcte_map<N, BPP, SEM>), grid, dim3(Geo<N, SEM>::T), 0, s, p);
     return hipGetLastError();
 }
@@ -1952,7 +1951,7 @@ static hipError_t launch_map_n(int bpp, int sem, const MapParams& p, hipStream_t
 
 hipError_t launch_map(int n, int bpp, int sem, const MapParams& p, hipStream_t s)
 {
-    if (p.y1 <= p.y0) return hipSuccess;
+    if (p.tiles_y <= 0) return hipSuccess;
     switch (n) {
     case 2: return launch_map_n<2>(bpp, sem, p, s);
     case 4: return launch_map_n<4>(bpp, sem, p, s);
@@ -1983,7 +1982,7 @@ static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
 {
     if (p.m.tile_h < 1 || p.tile_w != map_tile_w(N) || p.tiles_x != (p.m.w + p.tile_w - 1) / p.tile_w)
         return hipErrorInvalidValue;
-    const int nstrips = p.tiles_x * map_strips_per_tile(N) * ((p.m.y1 - p.m.y0 + p.m.tile_h - 1) / p.m.tile_h);
+    const int nstrips = p.tiles_x * map_strips_per_tile(N) * p.m.tiles_y;
     // one wave per block, as many as the device holds at once (LDS-bound:
     // ~10 per CU at N = 8 RGB); each walks the dirty list in strip batches.
     // Cached per device (CU counts may differ between devices).
@@ -2040,7 +2039,7 @@ static hipError_t launch_fix_tiles_n(int bpp, int sem, const TileFixParams& p, h
 
 hipError_t launch_fix_tiles(int n, int bpp, int sem, const TileFixParams& p, hipStream_t s)
 {
-    if (p.m.y1 <= p.m.y0) return hipSuccess;
+    if (p.m.tiles_y <= 0) return hipSuccess;
     switch (n) {
     case 2: return launch_fix_tiles_n<2>(bpp, sem, p, s);
     case 4: return launch_fix_tiles_n<4>(bpp, sem, p, s);

@@ -43,7 +43,7 @@ DCTE_CREATE_SAME_DEVICE = 1
 # every symbol include/dctenergy.h declares
 EXPORTS = ("dcte_abi_version", "dcte_device_count", "dcte_create", "dcte_destroy",
            "dcte_ctx_devices", "dcte_set_option", "dcte_energy_map",
-           "dcte_energy_map_device", "dcte_last_refined", "dcte_profile_read", "dcte_strerror",
+           "dcte_energy_map_device", "dcte_energy_map_device2", "dcte_last_refined", "dcte_profile_read", "dcte_strerror",
            "dcte_last_error", "dcte_normalize_u8", "dcte_energy_image_u8", "dcte_minmax_device",
            "dcte_normalize_u8_device", "dcte_seam_carve_device", "dcte_energy_points",
            "dcte_energy_points_device", "dcte_seam_find_device", "dcte_seam_find",
@@ -113,6 +113,12 @@ def lib():
                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                          ctypes.c_float, ctypes.c_int, vp, ctypes.c_longlong, vp]
+    L.dcte_energy_map_device2.restype = ctypes.c_int
+    L.dcte_energy_map_device2.argtypes = [vp, ctypes.c_int, vp, ctypes.c_longlong, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_int,
+                                          vp, ctypes.c_longlong, vp]
     L.dcte_last_refined.restype = ctypes.c_longlong
     L.dcte_last_refined.argtypes = [vp]
     L.dcte_profile_read.restype = ctypes.c_int
@@ -324,6 +330,16 @@ class Context:
         self._check(lib().dcte_energy_map_device(
             self._h, device, ctypes.c_void_p(d_px), rowstride, w, h, bpp, in_row0, in_rows,
             y0, y1, n, edges, textures, semantics, ctypes.c_void_p(d_out), out_stride,
+            ctypes.c_void_p(stream)))
+
+    def energy_map_device2(self, d_px, rowstride, w, h, bpp, in_row0, in_rows, y0, y1, yb0, yb1,
+                           n, edges, textures, d_out, out_stride, stream=0, device=0,
+                           semantics=DCTE_LQR):
+        """Rows [y0, y1) and [yb0, yb1) in one map launch (a band's two edge
+        ranges); row y of either at d_out + (y - y0) * out_stride."""
+        self._check(lib().dcte_energy_map_device2(
+            self._h, device, ctypes.c_void_p(d_px), rowstride, w, h, bpp, in_row0, in_rows,
+            y0, y1, yb0, yb1, n, edges, textures, semantics, ctypes.c_void_p(d_out), out_stride,
             ctypes.c_void_p(stream)))
 
     def energy_map_tensor(self, px, out, n=8, edges=0.5, textures=0.5, h=None, in_row0=0,

@@ -150,6 +150,17 @@ int dcte_energy_map_device(dcte_ctx *ctx, int device, const void *d_px,
                            float edges, float textures, int semantics, float *d_out,
                            long long out_stride, void *stream);
 
+/* The same for TWO output row ranges in one map launch and one refinement
+ * launch: [y0, y1) and [yb0, yb1) with y1 <= yb0 (yb0 == yb1: the second is
+ * empty); row y of either at d_out + (y - y0) * out_stride.  For a row-band
+ * shard: both halo-dependent edge ranges of a band after the
+ * RCCL halo exchange (the rows the clamp reaches for BOTH ranges readable). */
+int dcte_energy_map_device2(dcte_ctx *ctx, int device, const void *d_px,
+                            long long rowstride, int w, int h, int bpp,
+                            int in_row0, int in_rows, int y0, int y1, int yb0, int yb1,
+                            int n, float edges, float textures, int semantics,
+                            float *d_out, long long out_stride, void *stream);
+
 /* ---- seam carving support --------------------------------
  * After the initial map, liblqr carves one seam at a time and re-evaluates
  * the callback (src/render.c:134-157) only around the removed seam

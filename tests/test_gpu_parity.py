@@ -139,6 +139,68 @@ def test_device_bands_compose_bit_exact(ctx):
         assert torch.equal(full, parts), n
 
 
+def test_two_range_launch_equals_full_map(ctx):
+    """dcte_energy_map_device2 (a band's two halo-dependent edge ranges in ONE
+    map launch + ONE refinement launch) writes exactly the full map's rows of
+    both ranges and nothing else: natural and tie-dense (line-art) frames,
+    every N, both semantics, ranges from one row to more than a tile."""
+    torch = _torch()
+    from dctenergy import synth
+    H, W = 600, 517
+    nat = synth.natural_rows(0, H, W, 3, seed=6, device="cuda")
+    yy = torch.arange(H, device="cuda").view(-1, 1)
+    xx = torch.arange(W, device="cuda").view(1, -1)
+    line = torch.where((yy % 23 == 0) | (xx % 31 == 0) | ((xx + 2 * yy) % 97 == 0), 0, 255)
+    art = line.to(torch.uint8).unsqueeze(-1).expand(H, W, 3).contiguous()
+    cases = [(0, 3, 596, 600), (100, 104, 300, 303), (0, 1, 599, 600), (10, 150, 200, 480),
+             (50, 60, 60, 70), (5, 9, 9, 9)]
+    for frame in (nat, art):
+        for sem in (dctenergy.DCTE_LQR, dctenergy.DCTE_PREVIEW):
+            for n in (2, 4, 8, 16):
+                full = torch.empty((H, W), dtype=torch.float32, device="cuda")
+                ctx.energy_map_tensor(frame, full, n, 0.3, 0.7, semantics=sem)
+                for a0, a1, b0, b1 in cases:
+                    got = torch.full((H, W), -1.0, dtype=torch.float32, device="cuda")
+                    ctx.energy_map_device2(frame.data_ptr(), frame.stride(0), W, H, 3, 0, H, a0, a1,
+                                           b0, b1, n, 0.3, 0.7, got[a0:].data_ptr(), got.stride(0),
+                                           torch.cuda.current_stream().cuda_stream, semantics=sem)
+                    torch.cuda.synchronize()
+                    want = torch.full((H, W), -1.0, dtype=torch.float32, device="cuda")
+                    want[a0:a1] = full[a0:a1]
+                    want[b0:b1] = full[b0:b1]
+                    assert torch.equal(got, want), (n, sem, (a0, a1, b0, b1))
+
+
+def test_two_range_launch_band_buffer(ctx):
+    """The same from a band buffer holding only the rows the clamp reaches
+    (what a rank holds after the halo exchange), and the error for a second
+    range that overlaps the first."""
+    torch = _torch()
+    from dctenergy import synth
+    H, W = 2048, 1031
+    frame = synth.natural_rows(0, H, W, 3, seed=7, device="cuda")
+    for n in (8, 16):
+        r = n // 2
+        full = torch.empty((H, W), dtype=torch.float32, device="cuda")
+        ctx.energy_map_tensor(frame, full, n, 0.3, 0.7)
+        Y0, Y1 = 512, 1024
+        lo, hi = Y0 - (r - 1), Y1 - 1 + r
+        band = frame[lo:hi + 1].clone()
+        out = torch.full((Y1 - Y0, W), -1.0, dtype=torch.float32, device="cuda")
+        st = torch.cuda.current_stream().cuda_stream
+        ctx.energy_map_device(band.data_ptr(), band.stride(0), W, H, 3, lo, band.shape[0],
+                              Y0 + r - 1, Y1 - r, n, 0.3, 0.7, out[r - 1:].data_ptr(), out.stride(0), st)
+        ctx.energy_map_device2(band.data_ptr(), band.stride(0), W, H, 3, lo, band.shape[0],
+                               Y0, Y0 + r - 1, Y1 - r, Y1, n, 0.3, 0.7, out.data_ptr(), out.stride(0), st)
+        torch.cuda.synchronize()
+        assert torch.equal(out, full[Y0:Y1]), n
+        with pytest.raises(dctenergy.DcteError) as ei:
+            ctx.energy_map_device2(band.data_ptr(), band.stride(0), W, H, 3, lo, band.shape[0],
+                                   Y0, Y0 + 10, Y0 + 5, Y0 + 20, n, 0.3, 0.7, out.data_ptr(),
+                                   out.stride(0), st)
+        assert ei.value.code == dctenergy.DCTE_EINVAL
+
+
 def _compare_full(got_dev, ref, e, t, what):
     """Whole-frame comparison on the device, in row chunks: every pixel within
     the tolerance, and the class flips (a pixel whose value is the OTHER
