@@ -57,6 +57,8 @@ def main():
     ap.add_argument("--textures", type=float, default=0.7)
     ap.add_argument("--lib", default=None, help="libdctenergy_hip.so to load (A/B)")
     ap.add_argument("--frames", default="", help="comma-separated frame-name prefixes (default: all)")
+    ap.add_argument("--tau", type=float, default=4e-6,
+                    help="tie_tau of the timed calls (1 = every pixel refined: the exact mode)")
     a = ap.parse_args()
     if a.lib:
         os.environ["DCTE_LIB"] = os.path.abspath(a.lib)
@@ -96,16 +98,16 @@ def main():
             ms_off, ms_all, ms_kern = 1e9, 1e9, 1e9
             for _ in range(3):
                 ms_off = min(ms_off, timed(0.0)[0])
-                tot, kern = timed(4e-6)
+                tot, kern = timed(a.tau)
                 ms_all, ms_kern = min(ms_all, tot), min(ms_kern, kern)
             ms_map = ms_kern
-            ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, 4e-6)
+            ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, a.tau)
             # flagged count: the host entry point reports it (same kernels)
             host = fr.cpu().numpy()
             ctx.energy_map(host, n, e, t)
             flagged = ctx.last_refined
             del host
-            res = {"frame": name, "size": S, "n": n, "lib": os.path.basename(dctenergy.LIB_PATH),
+            res = {"frame": name, "size": S, "n": n, "tau": a.tau, "lib": os.path.basename(dctenergy.LIB_PATH),
                    "flagged": flagged,
                    "flagged_frac": round(flagged / (S * S), 5),
                    "map_ms": round(ms_map, 4), "map_plus_fix_ms": round(ms_all, 4),
