@@ -117,6 +117,7 @@ struct dcte_ctx {
     bool dp_bandwise = false;       // DCTE_OPT_DP_BANDWISE
     unsigned dp_spin_limit = 0;     // DCTE_OPT_DP_SPIN_LIMIT (0: the kernel's default)
     unsigned long long* stamps = nullptr;   // DCTE_OPT_TSTAMP_BUF (timing-probe builds)
+    int fail_inject = 0;            // DCTE_OPT_FAIL_INJECT (tests of the error paths)
     std::vector<ProfEvent> prof;
     long long last_refined = 0;
     std::string last_error;
@@ -395,9 +396,17 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     } else if ((e = dcte::launch_map(n, bpp, sem, p, s)) != hipSuccess) {
         return fail(e, "launch_map");
     }
+    // testing (DCTE_OPT_FAIL_INJECT): the launch was queued, report it failed
+    auto injected = [&](int which) {
+        if (ctx->fail_inject != which) return false;
+        ctx->fail_inject = 0;
+        return true;
+    };
+    if (injected(1)) return fail(hipErrorLaunchFailure, "launch_map (injected)");
     f->phase ^= 1u;   // the launch ran: the next one uses the counter it zeroed
     if ((p.we != p.wt && ctx->tie_tau > 0) || ctx->tie_tau >= 1.0) {
         if ((e = dcte::launch_fix_tiles(n, bpp, sem, q, s)) != hipSuccess) return fail(e, "launch_fix_tiles");
+        if (injected(2)) return fail(hipErrorLaunchFailure, "launch_fix_tiles (injected)");
     }
     return DCTE_OK;
 }
@@ -695,6 +704,10 @@ int dcte_set_option(dcte_ctx* ctx, int option, double value)
         // a device address (exact in a double below 2^53); 0 = none
         if (!(value >= 0 && value < 9007199254740992.0)) return DCTE_EINVAL;
         ctx->stamps = reinterpret_cast<unsigned long long*>((uintptr_t)value);
+        return DCTE_OK;
+    case DCTE_OPT_FAIL_INJECT:
+        if (!(value == 0 || value == 1 || value == 2)) return DCTE_EINVAL;
+        ctx->fail_inject = (int)value;
         return DCTE_OK;
     default: return DCTE_EINVAL;
     }

@@ -877,6 +877,17 @@ __device__ __forceinline__ void refine_group(const double* lum, int LW, int at, 
                       w, l, best, edge);
 }
 
+// The dense walks' waves: up to DCTE_DENSE_OVERSUB x the resident wave slots
+// (N = 8: one wave per dirty strip; N = 16: one per 16-entry batch up to that
+// cap), so the hardware hands out strips as slots free up instead of each
+// resident wave striding over a fixed tenth of them -- the launch's tail is one
+// strip.  16 vs 1 (r03): line art RGB 0.436 -> 0.393 ms, the 8-px grid 3.44 ->
+// 2.86, dots -10 %, N = 16 line art RGB 0.760 -> 0.695 (profiles/r04/
+// dense_oversub_ab.jsonl).  Splitting a strip into interleaved pieces, or the
+// same for the sparse walk, measured slower (dense_oversub_ab2.jsonl).
+#ifndef DCTE_DENSE_OVERSUB
+#define DCTE_DENSE_OVERSUB 16
+#endif
 // grey layers at N <= 4 fit 128 VGPRs: 4 waves per SIMD (the LDS allows them)
 #ifndef DCTE_FIX_MINW
 #define DCTE_FIX_MINW 4
@@ -2013,7 +2024,8 @@ static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
         const long long most = kDenseFlat<N, SEM>
                                    ? ((long long)nstrips * 64 * p.m.tile_h + kDenseBatch16 - 1) / kDenseBatch16
                                    : nstrips;
-        const int dblocks = most < resident ? (int)most : resident;
+        const long long dmax = (long long)resident * DCTE_DENSE_OVERSUB;
+        const int dblocks = (int)(most < dmax ? most : dmax);
         TileFixParams q = p;
         q.sparse_blocks = blocks;
         hipLaunchKernelGGL((dcte_fix_strips<N, BPP, SEM>), dim3(blocks + dblocks), dim3(64), 0, s, q);

@@ -36,6 +36,7 @@ DCTE_OPT_TILE_H = 4
 DCTE_OPT_DP_BANDWISE = 5
 DCTE_OPT_DP_SPIN_LIMIT = 6
 DCTE_OPT_TSTAMP_BUF = 7
+DCTE_OPT_FAIL_INJECT = 8
 DCTE_NORM_LQR = 0
 DCTE_NORM_PREVIEW = 1
 DCTE_CREATE_SAME_DEVICE = 1

@@ -96,6 +96,10 @@ extern "C" {
                                only: device address of a buffer of 3 uint64
                                per map workgroup {start, end, HW_ID}; 0 = none.
                                Product builds ignore it. */
+#define DCTE_OPT_FAIL_INJECT 8 /* testing the error paths: 1 = the next map
+                               launch is reported as failed (DCTE_EHIP) right
+                               after it was queued; 2 = the next refinement
+                               launch likewise.  One-shot; 0 = off. */
 
 typedef struct dcte_ctx dcte_ctx;
 

@@ -626,3 +626,38 @@ def test_failed_call_then_good_call(ctx):
         ctx.energy_map_tensor(frame, after, 8, 0.3, 0.7)
         torch.cuda.synchronize()
         assert torch.equal(after, before)
+
+
+@pytest.mark.parametrize("which", [1, 2])
+@pytest.mark.parametrize("n", [8, 16])
+def test_injected_launch_failure_then_good_call(ctx, which, n):
+    """a launch that fails AFTER the profiling events and the map
+    launch were queued (DCTE_OPT_FAIL_INJECT: 1 = reported after the map
+    launch, 2 = after the refinement launch) takes the error path that zeroes
+    both dirty counters on the stream and does not flip the counter phase;
+    the next calls on the same stream give the same bits as before."""
+    torch = _torch()
+    rng = np.random.default_rng(18)
+    img = (rng.random((200, 333)) < 0.03).astype(np.uint8) * 255      # tie-dense: refinement runs
+    frame = torch.from_numpy(img).cuda()
+    before = torch.empty((200, 333), dtype=torch.float32, device="cuda")
+    ctx.energy_map_tensor(frame, before, n, 0.3, 0.7)
+    torch.cuda.synchronize()
+    _assert_tol(before.cpu().numpy(), O.energy_map(img, n, 0.3, 0.7), "before")
+    for profile in (0, 1):
+        ctx.set_option(dctenergy.DCTE_OPT_PROFILE, profile)
+        try:
+            ctx.set_option(dctenergy.DCTE_OPT_FAIL_INJECT, which)
+            junk = torch.empty_like(before)
+            with pytest.raises(dctenergy.DcteError) as e:
+                ctx.energy_map_tensor(frame, junk, n, 0.3, 0.7)
+            assert e.value.code == dctenergy.DCTE_EHIP
+        finally:
+            ctx.set_option(dctenergy.DCTE_OPT_FAIL_INJECT, 0)
+            ctx.set_option(dctenergy.DCTE_OPT_PROFILE, 0)
+            ctx.profile_read()
+        for _ in range(2):
+            after = torch.full_like(before, -1.0)
+            ctx.energy_map_tensor(frame, after, n, 0.3, 0.7)
+            torch.cuda.synchronize()
+            assert torch.equal(after, before), (which, profile)

@@ -36,6 +36,7 @@ KNOBS = {
     "DCTE_FIX_MINW_LANES": ("dcte_kernels.hip", "3"),
     "DCTE_DENSE8_RB": ("dcte_kernels.hip", "4"),
     "DCTE_DENSE_CHUNK": ("dcte_kernels.hip", "8"),
+    "DCTE_DENSE_OVERSUB": ("dcte_kernels.hip", "1"),
     "DCTE_SHIFT_VEC": ("dcte_seam.hip", "1"),
     "DCTE_DP_C": ("dcte_dp.hip", "1"),
     "DCTE_DP_R": ("dcte_dp.hip", "16"),
