@@ -913,7 +913,10 @@ constexpr int kFixMinWaves = (BPP == 1 && N <= 8) ? (N == 8 ? DCTE_FIX_MINW_LANE
 #define DCTE_DENSE8_RB 8      // window rows per load batch
 #endif
 // the 256 liblqr channel quotients v / 255 (pre-weighted per channel for
-// liblqr RGB: kTab), as the reference divides (bit-identical)
+// liblqr RGB: kTab), as the reference divides (bit-identical); kTab also
+// fills lut[768 + v] = the luma of the grey pixel (v, v, v), summed in the
+// reference's order ((k_r v + k_g v) + k_b v): what the three tables give for
+// it, bit for bit (the dense N = 8 walk's grey-RGB path)
 template <bool kTab>
 __device__ __forceinline__ void fill_luma_lut(double* lut, int lane)
 {
@@ -925,10 +928,28 @@ __device__ __forceinline__ void fill_luma_lut(double* lut, int lane)
             lut[v] = 0.2126 * q;
             lut[256 + v] = 0.7152 * q;
             lut[512 + v] = 0.0722 * q;
+            lut[768 + v] = lut[v] + lut[256 + v] + lut[512 + v];
         } else {
             lut[v] = q;
         }
     }
+}
+
+// RGB bytes of a window line (8 pixels in 6 dwords, wd): every pixel grey
+// (R = G = B)?  d = the stream XOR itself shifted by one byte; within each
+// pixel's three bytes the first two of d are zero iff the channels agree.
+template <int K>
+__device__ __forceinline__ bool rgb_line_grey(const uint32_t (&wd)[K])
+{
+    static_assert(K % 3 == 0, "whole pixels: 4 per 3 dwords");
+    constexpr uint32_t M[3] = {0xFF00FFFFu, 0xFFFF00FFu, 0x00FFFF00u};
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+        const uint32_t nx = __builtin_amdgcn_alignbyte(j < K - 1 ? wd[j + 1] : 0u, wd[j], 1u);
+        acc |= (wd[j] ^ nx) & M[j % 3];
+    }
+    return acc == 0u;
 }
 
 // The dense-strip walk of one wave: wave `blk` of `nblk` takes dirty strips
@@ -998,6 +1019,22 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
                     for (int j = 0; j < NW; j++)
                         fv[rr][j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * j), 0, 0);
                 }
+                // liblqr RGB: when every window pixel of the batch's rows in
+                // every lane is grey (scanned documents, line art stored as
+                // RGB), one table read per element (lut[768 + v], the same
+                // double the three reads and two adds give) instead of three
+                bool grey = false;
+                if constexpr (SEM == kSemLqr && BPP == 3) {
+                    bool mine = true;
+#pragma unroll
+                    for (int rr = 0; rr < RB; rr++) {
+                        uint32_t wd[6];
+#pragma unroll
+                        for (int j = 0; j < 6; j++) wd[j] = __builtin_amdgcn_alignbyte(fv[rr][j + 1], fv[rr][j], foff[rr]);
+                        mine = mine && fast[rr] && rgb_line_grey(wd);
+                    }
+                    grey = __all(mine);                  // uniform
+                }
 #pragma unroll
                 for (int rr = 0; rr < RB; rr++) {
                     const int r = r0 + rr;
@@ -1007,11 +1044,15 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
 #pragma unroll
                         for (int j = 0; j < NW - 1; j++)
                             wd[j] = __builtin_amdgcn_alignbyte(fv[rr][j + 1], fv[rr][j], foff[rr]);
+                        auto byte = [&](int b) { return (wd[b >> 2] >> (8 * (b & 3))) & 255u; };
+                        if (grey) {
 #pragma unroll
-                        for (int c = 0; c < 8; c++) {
-                            auto byte = [&](int b) { return (wd[b >> 2] >> (8 * (b & 3))) & 255u; };
-                            lv[c] = luma3(byte(c * BPP), BPP > 1 ? byte(c * BPP + 1) : 0u,
-                                          BPP > 1 ? byte(c * BPP + 2) : 0u);
+                            for (int c = 0; c < 8; c++) lv[c] = lut[768 + byte(c * BPP)];
+                        } else {
+#pragma unroll
+                            for (int c = 0; c < 8; c++)
+                                lv[c] = luma3(byte(c * BPP), BPP > 1 ? byte(c * BPP + 1) : 0u,
+                                              BPP > 1 ? byte(c * BPP + 2) : 0u);
                         }
                     } else {
                         // clamped at the left / right frame border, or at the
@@ -1244,6 +1285,22 @@ __device__ __forceinline__ void fix_dense16_flat(const TileFixParams& tp, const 
     // X[K][kk][jj] = luma of line jj, pixel 4K + kk (the first index)
     auto convert = [&](const D16Rows<BPP>& R, double (&X)[4][4][4]) {
         const int gx0 = R.x - HL;
+        // RGB: every pixel of every lane's lines grey (R = G = B) -> one
+        // table read per element (lut[768 + v], the same double as the
+        // three reads and two adds; fill_luma_lut) instead of three
+        bool grey = false;
+        if constexpr (BPP == 3) {
+            bool mine = true;
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++) {
+                const uint32_t fo = (R.foff >> (2 * jj)) & 3u;
+                uint32_t wd[12];
+#pragma unroll
+                for (int j = 0; j < 12; j++) wd[j] = __builtin_amdgcn_alignbyte(R.fv[jj][j + 1], R.fv[jj][j], fo);
+                mine = mine && ((((R.fast >> jj) & 1u) && rgb_line_grey(wd)) || !R.valid);
+            }
+            grey = __all(mine);                          // uniform
+        }
 #pragma unroll
         for (int jj = 0; jj < 4; jj++) {
             double lv[16];
@@ -1253,10 +1310,14 @@ __device__ __forceinline__ void fix_dense16_flat(const TileFixParams& tp, const 
                 uint32_t wd[NW - 1];
 #pragma unroll
                 for (int j = 0; j < NW - 1; j++) wd[j] = __builtin_amdgcn_alignbyte(R.fv[jj][j + 1], R.fv[jj][j], fo);
+                auto byte = [&](int b) { return (wd[b >> 2] >> (8 * (b & 3))) & 255u; };
+                if (grey) {
 #pragma unroll
-                for (int c = 0; c < 16; c++) {
-                    auto byte = [&](int b) { return (wd[b >> 2] >> (8 * (b & 3))) & 255u; };
-                    lv[c] = luma3(byte(c * BPP), BPP > 1 ? byte(c * BPP + 1) : 0u, BPP > 1 ? byte(c * BPP + 2) : 0u);
+                    for (int c = 0; c < 16; c++) lv[c] = lut[768 + byte(c * BPP)];
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 16; c++)
+                        lv[c] = luma3(byte(c * BPP), BPP > 1 ? byte(c * BPP + 1) : 0u, BPP > 1 ? byte(c * BPP + 2) : 0u);
                 }
             } else {
                 // clamped at the left / right border, or at the frame's last
@@ -1390,7 +1451,7 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
     // staging here, and the N = 16 RGB dense blocks want pre-weighted tables
     constexpr bool kOwn = kDenseOwn<N, SEM>;
     constexpr bool kTab16 = N == 16 && kOwn && BPP == 3;
-    __shared__ double lut[(kTab || kTab16) ? 3 * 256 : 256];
+    __shared__ double lut[(kTab || kTab16) ? 4 * 256 : 256];
     __shared__ double lum[(kOtf || kOwn) ? 1 : LR * LW];   // fp64 luma of one band (+ halo), needed columns
     __shared__ unsigned char mis[LR];                  // byte offset of each raw row's first pixel
     __shared__ unsigned char colidx[(kOtf || kOwn) ? 1 : LW];   // the needed luma columns, ascending

@@ -575,6 +575,37 @@ def test_energy_windows_bit_exact(ctx, n):
         assert np.array_equal(got, ref), n
 
 
+@pytest.mark.parametrize("n", [8, 16])
+def test_grey_rgb_refinement_paths(n):
+    """The dense refinement walks read liblqr RGB luma through one table when
+    every pixel of a batch's windows is grey (R = G = B) and through three
+    otherwise: grey line art, line art whose strokes alternate between grey
+    and colour (batches mixing both kinds of lane), random RGB with a few
+    grey pixels, and a near-grey frame (one channel off by one) -- every
+    pixel refined (tie_tau = 1): bit-identical to the oracle, one and many
+    tile heights."""
+    rng = np.random.default_rng(90 + n)
+    H, W = 203, 333
+    yy, xx = np.ogrid[0:H, 0:W]
+    ink = (yy % 11 == 0) | (xx % 13 == 0) | ((xx + 2 * yy) % 37 == 0)
+    grey = np.repeat(np.where(ink, 0, 255).astype(np.uint8)[..., None], 3, -1)
+    mixed = grey.copy()
+    mixed[(xx % 26 == 0) & (yy >= 0)] = (200, 30, 30)
+    rnd = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    rnd[rng.random((H, W)) < 0.2] = 77
+    near = grey.copy()
+    near[..., 2] ^= (rng.random((H, W)) < 0.01).astype(np.uint8)
+    with dctenergy.Context(ngpus=1, tie_tau=1.0) as c:
+        for th in (0, 16):
+            c.set_option(dctenergy.DCTE_OPT_TILE_H, th)
+            for name, img in (("grey", grey), ("mixed", mixed), ("random", rnd), ("near", near)):
+                got = c.energy_map(img, n, 0.3, 0.7)
+                assert np.array_equal(got, O.energy_map(img, n, 0.3, 0.7)), (n, th, name)
+    with dctenergy.Context(ngpus=1) as c:           # the default tau: the tie-dense strips
+        for name, img in (("grey", grey), ("mixed", mixed)):
+            _assert_tol(c.energy_map(img, n, 0.3, 0.7), O.energy_map(img, n, 0.3, 0.7), name)
+
+
 @pytest.mark.parametrize("n", [2, 4, 8, 16])
 def test_refine_all_bit_exact_every_layout(n):
     """tie_tau >= 1 sends every pixel through dcte_fix_strips (dense strips:

@@ -39,6 +39,9 @@ def frames(S, torch, dev):
         "uniform_rgb": torch.randint(0, 256, (S, S, 3), generator=g, device=dev, dtype=torch.uint8),
         "lineart_grey": white(line),
         "lineart_rgb": rgb(white(line)),
+        # the same strokes in colour (R != G): the refinement's three-table luma path
+        "lineart_color": torch.where(line.unsqueeze(-1), torch.tensor([200, 30, 30], dtype=torch.uint8, device=dev),
+                                     torch.tensor([255, 255, 255], dtype=torch.uint8, device=dev)).contiguous(),
         "grid8_grey": white(grid8),
         "dots64_grey": torch.where(dots, 255, 16).to(torch.uint8),
         "dots64_rgb": rgb(torch.where(dots, 255, 16).to(torch.uint8)),
