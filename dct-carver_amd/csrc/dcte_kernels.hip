@@ -895,8 +895,12 @@ __device__ __forceinline__ void refine_group(const double* lum, int LW, int at, 
 #ifndef DCTE_FIX_MINW_LANES
 #define DCTE_FIX_MINW_LANES 2   // N = 8 (lane-per-pixel dense strips in the same launch): the window alone is 128 VGPRs
 #endif
+#ifndef DCTE_FIX_MINW_RGB8
+#define DCTE_FIX_MINW_RGB8 1    // N = 8 RGB layers
+#endif
 template <int N, int BPP>
-constexpr int kFixMinWaves = (BPP == 1 && N <= 8) ? (N == 8 ? DCTE_FIX_MINW_LANES : DCTE_FIX_MINW) : 1;
+constexpr int kFixMinWaves = (BPP == 1 && N <= 8) ? (N == 8 ? DCTE_FIX_MINW_LANES : DCTE_FIX_MINW)
+                                                  : (N == 8 && BPP == 3 ? DCTE_FIX_MINW_RGB8 : 1);
 
 // Dense strips at N = 8 (more than kFixDirect<8> flagged pixels; the sparse
 // ones stay with dcte_fix_strips): one lane per flagged pixel, its whole
@@ -909,9 +913,6 @@ constexpr int kFixMinWaves = (BPP == 1 && N <= 8) ? (N == 8 ? DCTE_FIX_MINW_LANE
 // (line art RGB at 16384^2: 1.27 -> 0.46 ms, profiles/r03/fix_lanes_ab.jsonl).
 // Extra blocks of the dcte_fix_strips launch: no band staging, so only the
 // tables take LDS.  Waves take dirty strips in turn.
-#ifndef DCTE_DENSE8_RB
-#define DCTE_DENSE8_RB 8      // window rows per load batch
-#endif
 // the 256 liblqr channel quotients v / 255 (pre-weighted per channel for
 // liblqr RGB: kTab), as the reference divides (bit-identical); kTab also
 // fills lut[768 + v] = the luma of the grey pixel (v, v, v), summed in the
@@ -952,14 +953,51 @@ __device__ __forceinline__ bool rgb_line_grey(const uint32_t (&wd)[K])
     return acc == 0u;
 }
 
+// Window memo of the dense N = 8 walk (r04).  Tie-dense frames are regular:
+// their flagged windows repeat (straight strokes, grid lines, flat fills, the
+// same glyph), and a window's refined energy depends only on its bytes.  Each
+// wave keeps the windows it refined in an LDS table -- kMemoSlots entries,
+// direct-mapped on a hash of the key, key = the window's 64 bytes (liblqr /
+// preview grey; RGB: the R bytes of a window whose every pixel has R = G = B,
+// which then fix its luma) and the output's bits -- and answers a flagged pixel
+// whose window equals an entry's key in all 64 bytes from the entry.  Misses
+// queue in LDS and are refined 64 at a time, full waves across strip
+// boundaries.  Entries are written by one elected lane per slot and read only
+// after the wave's refinement phase, so none is ever seen half-written.
+// Grey layers only: for RGB (keyed by the R bytes of windows whose pixels are
+// all grey) the probe's second load of every miss and the extra registers
+// (2 waves per SIMD instead of 3) cost more than the hits saved -- grey line
+// art stored as RGB +28 %, colour strokes +40 % (profiles/r04/memo_ab.jsonl).
+constexpr int kMemoSlots = 64;
+constexpr int kMemoStride = 17;                        // 16 key dwords + the output's bits
+constexpr uint32_t kMemoEmpty = 0xFFFFFFFFu;           // a NaN: never an output
+constexpr int kMemoPend = 128;                         // misses waiting for a full batch (< 64 + 64)
+constexpr int kMemoDwords = kMemoSlots * kMemoStride + kMemoPend;
+
+// slot of a key: FNV-1a over its dwords, then a murmur finaliser, top bits.
+// (A rotate-xor fold is linear over GF(2) and maps the 0x00 / 0xFF byte
+// patterns of line art onto few slots.)
+__device__ __forceinline__ int memo_slot(const uint32_t (&key)[16])
+{
+    uint32_t h = 0x811c9dc5u;
+#pragma unroll
+    for (int j = 0; j < 16; j++) h = (h ^ key[j]) * 0x01000193u;
+    h ^= h >> 15;
+    h *= 0x2c1b3c6du;
+    h ^= h >> 12;
+    return (int)(h >> 26);                             // kMemoSlots = 64
+}
+
 // The dense-strip walk of one wave: wave `blk` of `nblk` takes dirty strips
-// blk, blk + nblk, ...; `lut` filled by fill_luma_lut.
+// blk, blk + nblk, ...; `lut` filled by fill_luma_lut; `memo` the wave's
+// kMemoDwords of LDS.
 template <int BPP, int SEM>
-__device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const double* lut,
+__device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const double* lut, uint32_t* memo,
                                                unsigned blk, unsigned nblk)
 {
     constexpr int N = 8;
     constexpr int HL = Geo<N, SEM>::HL;
+    constexpr bool kMemo = BPP == 1;                // grey layers (RGB: see below)
     const MapParams& p = tp.m;
     const unsigned ndirty = *p.dirty_count;
     const int lane = threadIdx.x;
@@ -981,101 +1019,256 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
     };
     const unsigned spt = (unsigned)tp.tile_w / 64u;   // strips per map tile
     constexpr int NW = (8 * BPP + 3) / 4 + 1;         // dwords of a row's 8 pixels, any alignment
-    for (unsigned k = blk; k < ndirty; k += nblk) {   // uniform
-        const unsigned strip = p.dirty_list[k];
-        const unsigned cnt = p.tile_count[strip];
-        if (cnt <= kFixDirect<N>) continue;            // sparse: dcte_fix_strips' own walk
-        const unsigned tile = strip / spt;
-        const int bx = (int)(tile % (unsigned)tp.tiles_x), by = (int)(tile / (unsigned)tp.tiles_x);
-        const int sx0 = bx * tp.tile_w + 64 * (int)(strip % spt);
-        const int ys = tile_row0(p, by);
-        const unsigned* list = p.fix_list + (size_t)strip * (size_t)(64 * p.tile_h);
-        for (unsigned q0 = 0; q0 < cnt; q0 += 64) {   // uniform
-            const unsigned q = q0 + (unsigned)lane;
-            if (q >= cnt) continue;
-            const unsigned loc = list[q];
-            const int lx = (int)(loc & 63), ly = (int)(loc >> 6);
-            const int x = sx0 + lx, y = ys + ly;
-            const int gx0 = x - HL;
-            const bool inside = gx0 >= 0 && gx0 + 8 <= p.w;
-            // rows in batches of RB: a batch's loads are issued, then its
-            // bytes converted
-            constexpr int RB = DCTE_DENSE8_RB;
-            double d[64];
+    uint32_t* const pend = memo + kMemoSlots * kMemoStride;
+    if constexpr (kMemo) {
+        for (int s = lane; s < kMemoSlots; s += 64) memo[s * kMemoStride + 16] = kMemoEmpty;
+        wave_sync_lds();
+    }
+
+    // the window's eight image rows as whole dwords (fast: unclamped and
+    // inside the buffer; otherwise the loads return zeros)
+    auto load_rows = [&](bool active, int x, int y, uint32_t (&fv)[8][NW], uint32_t (&foff)[8], bool (&fast)[8]) {
+        const int gx0 = x - HL;
+        const bool inside = active && gx0 >= 0 && gx0 + 8 <= p.w;
 #pragma unroll
-            for (int r0 = 0; r0 < 8; r0 += RB) {
-                uint32_t fv[RB][NW];
-                uint32_t foff[RB];
-                bool fast[RB];
+        for (int rr = 0; rr < 8; rr++) {
+            const int gy = clampi(y - HL + rr, 0, p.h - 1);
+            const uint32_t s0 = base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
+                                (uint32_t)(gx0 * BPP);
+            fast[rr] = inside && ((s0 + 8 * BPP - 1) | 3u) < nrec;
+            foff[rr] = s0 & 3u;
+            const uint32_t a = fast[rr] ? (s0 & ~3u) : 0x7ffffff0u;   // past num_records: zeros
 #pragma unroll
-                for (int rr = 0; rr < RB; rr++) {
-                    const int gy = clampi(y - HL + r0 + rr, 0, p.h - 1);
-                    const uint32_t s0 = base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
-                                        (uint32_t)(gx0 * BPP);
-                    fast[rr] = inside && ((s0 + 8 * BPP - 1) | 3u) < nrec;
-                    foff[rr] = s0 & 3u;
-                    const uint32_t a = fast[rr] ? (s0 & ~3u) : 0x7ffffff0u;   // past num_records: zeros
+            for (int j = 0; j < NW; j++)
+                fv[rr][j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * j), 0, 0);
+        }
+    };
+    // the window's memo key; false: it has none (a clamped row, or RGB with a
+    // pixel whose channels differ)
+    auto make_key = [&](const uint32_t (&fv)[8][NW], const uint32_t (&foff)[8], const bool (&fast)[8],
+                        uint32_t (&key)[16]) -> bool {
+        bool ok = true;
 #pragma unroll
-                    for (int j = 0; j < NW; j++)
-                        fv[rr][j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * j), 0, 0);
+        for (int rr = 0; rr < 8; rr++) {
+            uint32_t wd[NW - 1];
+#pragma unroll
+            for (int j = 0; j < NW - 1; j++) wd[j] = __builtin_amdgcn_alignbyte(fv[rr][j + 1], fv[rr][j], foff[rr]);
+            ok = ok && fast[rr];
+            if constexpr (BPP == 1) {
+                key[2 * rr] = wd[0];
+                key[2 * rr + 1] = wd[1];
+            } else {
+                uint32_t g6[6];
+#pragma unroll
+                for (int j = 0; j < 6; j++) g6[j] = wd[j];
+                ok = ok && rgb_line_grey(g6);
+                auto byte = [&](int b) { return (wd[b >> 2] >> (8 * (b & 3))) & 255u; };
+                key[2 * rr] = byte(0) | byte(3) << 8 | byte(6) << 16 | byte(9) << 24;
+                key[2 * rr + 1] = byte(12) | byte(15) << 8 | byte(18) << 16 | byte(21) << 24;
+            }
+        }
+        return ok;
+    };
+
+    // refine the pixel of each active lane from its loaded rows (fp64, the
+    // reference's order) and, with `ins` (uniform), enter its window into the
+    // memo
+    auto refine_rows = [&](bool active, int x, int y, const uint32_t (&fv)[8][NW], const uint32_t (&foff)[8],
+                           const bool (&fast)[8], bool ins) {
+        if (!active) return;
+        int slot = -1;                                   // the memo slot this lane fills
+        if (kMemo && ins) {
+            uint32_t key[16];
+            const bool keyed = make_key(fv, foff, fast, key);
+            int s = 0;
+            if (keyed) {
+                s = memo_slot(key);
+                memo[s * kMemoStride + 16] = (uint32_t)lane;        // one lane per slot wins
+            }
+            wave_sync_lds();
+            if (keyed && memo[s * kMemoStride + 16] == (uint32_t)lane) {
+#pragma unroll
+                for (int j = 0; j < 16; j++) memo[s * kMemoStride + j] = key[j];
+                slot = s;                                // its value follows the refinement
+            }
+        }
+        // liblqr RGB: when every window pixel of every lane is grey (scanned
+        // documents, line art stored as RGB), one table read per element
+        // (lut[768 + v], the same double the three reads and two adds give)
+        // instead of three
+        bool grey = false;
+        if constexpr (SEM == kSemLqr && BPP == 3) {
+            bool mine = true;
+#pragma unroll
+            for (int rr = 0; rr < 8; rr++) {
+                uint32_t wd[6];
+#pragma unroll
+                for (int j = 0; j < 6; j++) wd[j] = __builtin_amdgcn_alignbyte(fv[rr][j + 1], fv[rr][j], foff[rr]);
+                mine = mine && fast[rr] && rgb_line_grey(wd);
+            }
+            grey = __all(mine);                  // uniform
+        }
+        double d[64];
+        const int gx0 = x - HL;
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            double lv[8];
+            if (fast[r]) {
+                uint32_t wd[NW - 1];
+#pragma unroll
+                for (int j = 0; j < NW - 1; j++) wd[j] = __builtin_amdgcn_alignbyte(fv[r][j + 1], fv[r][j], foff[r]);
+                auto byte = [&](int b) { return (wd[b >> 2] >> (8 * (b & 3))) & 255u; };
+                if (grey) {
+#pragma unroll
+                    for (int c = 0; c < 8; c++) lv[c] = lut[768 + byte(c * BPP)];
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 8; c++)
+                        lv[c] = luma3(byte(c * BPP), BPP > 1 ? byte(c * BPP + 1) : 0u, BPP > 1 ? byte(c * BPP + 2) : 0u);
                 }
-                // liblqr RGB: when every window pixel of the batch's rows in
-                // every lane is grey (scanned documents, line art stored as
-                // RGB), one table read per element (lut[768 + v], the same
-                // double the three reads and two adds give) instead of three
-                bool grey = false;
-                if constexpr (SEM == kSemLqr && BPP == 3) {
-                    bool mine = true;
+            } else {
+                // clamped at the left / right frame border, or at the frame's
+                // last bytes: per-pixel reads
+                const int gy = clampi(y - HL + r, 0, p.h - 1);
+                const uint8_t* row = p.px + (long long)(gy - p.in_row0) * p.rowstride;
 #pragma unroll
-                    for (int rr = 0; rr < RB; rr++) {
-                        uint32_t wd[6];
-#pragma unroll
-                        for (int j = 0; j < 6; j++) wd[j] = __builtin_amdgcn_alignbyte(fv[rr][j + 1], fv[rr][j], foff[rr]);
-                        mine = mine && fast[rr] && rgb_line_grey(wd);
-                    }
-                    grey = __all(mine);                  // uniform
-                }
-#pragma unroll
-                for (int rr = 0; rr < RB; rr++) {
-                    const int r = r0 + rr;
-                    double lv[8];
-                    if (fast[rr]) {
-                        uint32_t wd[NW - 1];
-#pragma unroll
-                        for (int j = 0; j < NW - 1; j++)
-                            wd[j] = __builtin_amdgcn_alignbyte(fv[rr][j + 1], fv[rr][j], foff[rr]);
-                        auto byte = [&](int b) { return (wd[b >> 2] >> (8 * (b & 3))) & 255u; };
-                        if (grey) {
-#pragma unroll
-                            for (int c = 0; c < 8; c++) lv[c] = lut[768 + byte(c * BPP)];
-                        } else {
-#pragma unroll
-                            for (int c = 0; c < 8; c++)
-                                lv[c] = luma3(byte(c * BPP), BPP > 1 ? byte(c * BPP + 1) : 0u,
-                                              BPP > 1 ? byte(c * BPP + 2) : 0u);
-                        }
-                    } else {
-                        // clamped at the left / right frame border, or at the
-                        // frame's last bytes: per-pixel reads
-                        const int gy = clampi(y - HL + r, 0, p.h - 1);
-                        const uint8_t* row = p.px + (long long)(gy - p.in_row0) * p.rowstride;
-#pragma unroll
-                        for (int c = 0; c < 8; c++) {
-                            const uint8_t* q8 = row + (long long)clampi(gx0 + c, 0, p.w - 1) * BPP;
-                            lv[c] = luma3(q8[0], BPP > 1 ? q8[1] : 0u, BPP > 1 ? q8[2] : 0u);
-                        }
-                    }
-                    // image row r, pixel c: liblqr data[c][r], preview data[r][c]
-#pragma unroll
-                    for (int c = 0; c < 8; c++) d[SEM == kSemLqr ? c * 8 + r : r * 8 + c] = lv[c];
+                for (int c = 0; c < 8; c++) {
+                    const uint8_t* q8 = row + (long long)clampi(gx0 + c, 0, p.w - 1) * BPP;
+                    lv[c] = luma3(q8[0], BPP > 1 ? q8[1] : 0u, BPP > 1 ? q8[2] : 0u);
                 }
             }
-            double m;
-            bool edge;
-            refine_regs<8>(d, tp.ct, m, edge);
-            p.out[(long long)(y - p.y0) * p.out_stride + x] =
-                edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
+            // image row r, pixel c: liblqr data[c][r], preview data[r][c]
+#pragma unroll
+            for (int c = 0; c < 8; c++) d[SEM == kSemLqr ? c * 8 + r : r * 8 + c] = lv[c];
         }
+        double m;
+        bool edge;
+        refine_regs<8>(d, tp.ct, m, edge);
+        const float v = edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
+        p.out[(long long)(y - p.y0) * p.out_stride + x] = v;
+        if (kMemo && slot >= 0) memo[slot * kMemoStride + 16] = __float_as_uint(v);
+    };
+
+    if constexpr (!kMemo) {
+        for (unsigned k = blk; k < ndirty; k += nblk) {   // uniform
+            const unsigned strip = p.dirty_list[k];
+            const unsigned cnt = p.tile_count[strip];
+            if (cnt <= kFixDirect<N>) continue;            // sparse: dcte_fix_strips' own walk
+            const unsigned tile = strip / spt;
+            const int bx = (int)(tile % (unsigned)tp.tiles_x), by = (int)(tile / (unsigned)tp.tiles_x);
+            const int sx0 = bx * tp.tile_w + 64 * (int)(strip % spt);
+            const int ys = tile_row0(p, by);
+            const unsigned* list = p.fix_list + (size_t)strip * (size_t)(64 * p.tile_h);
+            for (unsigned q0 = 0; q0 < cnt; q0 += 64) {   // uniform
+                const unsigned q = q0 + (unsigned)lane;
+                if (q >= cnt) continue;
+                const unsigned loc = list[q];
+                const int x = sx0 + (int)(loc & 63), y = ys + (int)(loc >> 6);
+                uint32_t fv[8][NW];
+                uint32_t foff[8];
+                bool fast[8];
+                load_rows(true, x, y, fv, foff, fast);
+                refine_rows(true, x, y, fv, foff, fast, false);
+            }
+        }
+        return;
+    } else {
+    // misses wait in pend[0 .. np) as (y - y0) * w + x (< 2^32: the launch's
+    // output span, checked by the host)
+    const unsigned uw = (unsigned)p.w;
+    unsigned np = 0;                                       // uniform
+    bool use = true;                                       // uniform: this wave's windows repeat
+    unsigned tries = 0, hits = 0;                          // uniform: windows probed, answered
+    // a step probes the current strip's next 64 entries and queues the misses
+    // (after 512 windows with fewer than one in eight answered, the wave
+    // queues without probing); a full batch of misses (at the end: what is
+    // left) is loaded again and refined.  One refinement site.
+    unsigned k = blk, q0 = 0, cnt = 0;                     // uniform
+    int sx0 = 0, ys = 0;
+    const unsigned* list = nullptr;
+    bool have = false;                                     // strip k has entries from q0 on
+    for (;;) {
+        while (!have && k < ndirty) {                      // uniform
+            const unsigned strip = p.dirty_list[k];
+            cnt = p.tile_count[strip];
+            if (cnt <= kFixDirect<N>) {                    // sparse: dcte_fix_strips' own walk
+                k += nblk;
+                continue;
+            }
+            const unsigned tile = strip / spt;
+            const int bx = (int)(tile % (unsigned)tp.tiles_x), by = (int)(tile / (unsigned)tp.tiles_x);
+            sx0 = bx * tp.tile_w + 64 * (int)(strip % spt);
+            ys = tile_row0(p, by);
+            list = p.fix_list + (size_t)strip * (size_t)(64 * p.tile_h);
+            q0 = 0;
+            have = true;
+        }
+        if (have && np < 64) {                             // uniform
+            const unsigned q = q0 + (unsigned)lane;
+            const bool act = q < cnt;
+            const unsigned loc = act ? list[q] : 0u;
+            const int x = sx0 + (int)(loc & 63), y = ys + (int)(loc >> 6);
+            bool hit = false;
+            if (use) {
+                uint32_t fv[8][NW];
+                uint32_t foff[8];
+                bool fast[8];
+                load_rows(act, x, y, fv, foff, fast);
+                uint32_t key[16];
+                if (act && make_key(fv, foff, fast, key)) {
+                    const uint32_t* ent = memo + memo_slot(key) * kMemoStride;
+                    const uint32_t val = ent[16];
+                    uint32_t diff = val == kMemoEmpty ? 1u : 0u;
+#pragma unroll
+                    for (int j = 0; j < 16; j++) diff |= ent[j] ^ key[j];
+                    if (diff == 0u) {
+                        p.out[(long long)(y - p.y0) * p.out_stride + x] = __uint_as_float(val);
+                        hit = true;
+                    }
+                }
+            }
+            const unsigned long long bal = __ballot(act && !hit);
+            if (act && !hit)
+                pend[np + (unsigned)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u))] =
+                    (uint32_t)(y - p.y0) * uw + (uint32_t)x;
+            const unsigned nmiss = (unsigned)__popcll(bal);
+            if (use) {
+                const unsigned nact = (unsigned)__popcll(__ballot(act));
+                tries += nact;
+                hits += nact - nmiss;
+                if (tries >= 512 && hits * 8 < tries) use = false;
+            }
+            np += nmiss;
+            wave_sync_lds();
+            q0 += 64u;
+            if (q0 >= cnt) {
+                have = false;
+                k += nblk;
+            }
+        }
+        const bool done = !have && k >= ndirty;
+        if (np >= 64 || (done && np > 0)) {                // refine pend[0 .. c)
+            const unsigned c = np >= 64 ? 64u : np;
+            const bool act = (unsigned)lane < c;
+            const uint32_t e = act ? pend[lane] : 0u;
+            wave_sync_lds();
+            if ((unsigned)lane < np - c) pend[lane] = pend[c + (unsigned)lane];   // the rest moves down
+            np -= c;
+            unsigned yr = (unsigned)((double)e / (double)uw);
+            if ((unsigned long long)yr * uw > e) yr--;     // the quotient rounded up
+            const int x = (int)(e - yr * uw), y = p.y0 + (int)yr;
+            if (act) {
+                uint32_t fv[8][NW];
+                uint32_t foff[8];
+                bool fast[8];
+                load_rows(true, x, y, fv, foff, fast);
+                refine_rows(true, x, y, fv, foff, fast, use);
+            }
+            wave_sync_lds();
+        }
+        if (done && np == 0) break;
+    }
     }
 }
 
@@ -1477,7 +1670,9 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
                 if (blk >= ndirty) return;             // uniform
                 fill_luma_lut<kTab>(lut, threadIdx.x);
                 wave_sync_lds();
-                fix_dense8_run<BPP, SEM>(tp, lut, blk, nblk);
+                // the window buffers of the sparse walk hold the dense walk's memo
+                static_assert(sizeof(rw_lds) >= kMemoDwords * sizeof(uint32_t), "memo fits");
+                fix_dense8_run<BPP, SEM>(tp, lut, reinterpret_cast<uint32_t*>(rw_lds), blk, nblk);
             } else {
                 fill_luma_lut<kTab16>(lut, threadIdx.x);
                 wave_sync_lds();

@@ -606,6 +606,40 @@ def test_grey_rgb_refinement_paths(n):
             _assert_tol(c.energy_map(img, n, 0.3, 0.7), O.energy_map(img, n, 0.3, 0.7), name)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [8, 16])
+def test_window_memo_near_duplicates(n):
+    """The dense walks answer a window whose bytes equal an earlier refined
+    window's from a per-wave memo.  Frames built to defeat a wrong key: strokes
+    of three inks (0, 1, 2) on a ground of 255 with 1-in-300 pixels at 254, so
+    most windows repeat and many differ from a repeated one in ONE byte; the
+    same as grey-valued RGB, as RGB whose G or B is off by one at 1-in-200
+    pixels (R alone would collide), and a frame whose strokes repeat exactly
+    along every row (all hits).  Every pixel refined (tie_tau = 1): liblqr and
+    preview maps bit-identical to the oracle, two tile heights."""
+    rng = np.random.default_rng(300 + n)
+    H, W = 257, 517
+    yy, xx = np.ogrid[0:H, 0:W]
+    ink = np.full((H, W), 255, np.uint8)
+    ink[rng.random((H, W)) < 1 / 300] = 254
+    for k, m in enumerate(((yy % 11 == 0) & (xx >= 0), (xx % 13 == 0) & (yy >= 0), (xx + 2 * yy) % 37 == 0)):
+        ink[m] = k
+    rgb = np.repeat(ink[..., None], 3, -1)
+    off = rgb.copy()
+    sel = rng.random((H, W)) < 1 / 200
+    off[sel, 1 + (rng.random(int(sel.sum())) < 0.5)] ^= 1
+    rows = np.repeat(np.where((yy % 7 == 0) | (yy % 7 == 3), 0, 255).astype(np.uint8), W, 1)
+    frames = (("grey", ink), ("rgb", rgb), ("off", off), ("rows", rows))
+    with dctenergy.Context(ngpus=1, tie_tau=1.0) as c:
+        for th in (0, 16):
+            c.set_option(dctenergy.DCTE_OPT_TILE_H, th)
+            for name, img in frames:
+                got = c.energy_map(img, n, 0.3, 0.7)
+                assert np.array_equal(got, O.energy_map(img, n, 0.3, 0.7)), (n, th, name, "liblqr")
+                got = c.energy_map(img, n, 0.3, 0.7, semantics=dctenergy.DCTE_PREVIEW)
+                assert np.array_equal(got, O.preview_map(img, n, 0.3, 0.7)), (n, th, name, "preview")
+
+
 @pytest.mark.parametrize("n", [2, 4, 8, 16])
 def test_refine_all_bit_exact_every_layout(n):
     """tie_tau >= 1 sends every pixel through dcte_fix_strips (dense strips:

@@ -34,7 +34,7 @@ KNOBS = {
     "DCTE_FIX_GPS": ("dcte_kernels.hip", "1"),
     "DCTE_FIX_MINW": ("dcte_kernels.hip", "3"),
     "DCTE_FIX_MINW_LANES": ("dcte_kernels.hip", "3"),
-    "DCTE_DENSE8_RB": ("dcte_kernels.hip", "4"),
+    "DCTE_FIX_MINW_RGB8": ("dcte_kernels.hip", "3"),
     "DCTE_DENSE_CHUNK": ("dcte_kernels.hip", "8"),
     "DCTE_DENSE_OVERSUB": ("dcte_kernels.hip", "1"),
     "DCTE_SHIFT_VEC": ("dcte_seam.hip", "1"),
