@@ -888,6 +888,13 @@ __device__ __forceinline__ void refine_group(const double* lum, int LW, int at, 
 #ifndef DCTE_DENSE_OVERSUB
 #define DCTE_DENSE_OVERSUB 16
 #endif
+// N = 8 grey layers (the window memo): fewer waves, each walking several
+// strips, keep their memo tables warm -- 4 vs 16: line art 0.283 -> 0.269 ms,
+// the 8-px grid 1.565 -> 1.49; 8, 2, 1 in between or slower
+// (profiles/r04/memo_oversub_ab.jsonl)
+#ifndef DCTE_DENSE_OVERSUB_MEMO
+#define DCTE_DENSE_OVERSUB_MEMO 4
+#endif
 // grey layers at N <= 4 fit 128 VGPRs: 4 waves per SIMD (the LDS allows them)
 #ifndef DCTE_FIX_MINW
 #define DCTE_FIX_MINW 4
@@ -2280,7 +2287,7 @@ static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
         const long long most = kDenseFlat<N, SEM>
                                    ? ((long long)nstrips * 64 * p.m.tile_h + kDenseBatch16 - 1) / kDenseBatch16
                                    : nstrips;
-        const long long dmax = (long long)resident * DCTE_DENSE_OVERSUB;
+        const long long dmax = (long long)resident * (N == 8 && BPP == 1 ? DCTE_DENSE_OVERSUB_MEMO : DCTE_DENSE_OVERSUB);
         const int dblocks = (int)(most < dmax ? most : dmax);
         TileFixParams q = p;
         q.sparse_blocks = blocks;

@@ -37,6 +37,7 @@ KNOBS = {
     "DCTE_FIX_MINW_RGB8": ("dcte_kernels.hip", "3"),
     "DCTE_DENSE_CHUNK": ("dcte_kernels.hip", "8"),
     "DCTE_DENSE_OVERSUB": ("dcte_kernels.hip", "1"),
+    "DCTE_DENSE_OVERSUB_MEMO": ("dcte_kernels.hip", "16"),
     "DCTE_SHIFT_VEC": ("dcte_seam.hip", "1"),
     "DCTE_DP_C": ("dcte_dp.hip", "1"),
     "DCTE_DP_R": ("dcte_dp.hip", "16"),
