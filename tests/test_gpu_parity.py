@@ -142,8 +142,9 @@ def test_device_bands_compose_bit_exact(ctx):
 def test_two_range_launch_equals_full_map(ctx):
     """dcte_energy_map_device2 (a band's two halo-dependent edge ranges in ONE
     map launch + ONE refinement launch) writes exactly the full map's rows of
-    both ranges and nothing else: natural and tie-dense (line-art) frames,
-    every N, both semantics, ranges from one row to more than a tile."""
+    both ranges and nothing else: natural and tie-dense (line-art, RGB and
+    grey) frames, every N, both semantics, ranges from one row to more than a
+    tile."""
     torch = _torch()
     from dctenergy import synth
     H, W = 600, 517
@@ -152,16 +153,18 @@ def test_two_range_launch_equals_full_map(ctx):
     xx = torch.arange(W, device="cuda").view(1, -1)
     line = torch.where((yy % 23 == 0) | (xx % 31 == 0) | ((xx + 2 * yy) % 97 == 0), 0, 255)
     art = line.to(torch.uint8).unsqueeze(-1).expand(H, W, 3).contiguous()
+    grey = line.to(torch.uint8).contiguous()       # grey: the N = 8 dense walk's window memo
     cases = [(0, 3, 596, 600), (100, 104, 300, 303), (0, 1, 599, 600), (10, 150, 200, 480),
              (50, 60, 60, 70), (5, 9, 9, 9)]
-    for frame in (nat, art):
+    for frame in (nat, art, grey):
+        bpp = 1 if frame.dim() == 2 else 3
         for sem in (dctenergy.DCTE_LQR, dctenergy.DCTE_PREVIEW):
             for n in (2, 4, 8, 16):
                 full = torch.empty((H, W), dtype=torch.float32, device="cuda")
                 ctx.energy_map_tensor(frame, full, n, 0.3, 0.7, semantics=sem)
                 for a0, a1, b0, b1 in cases:
                     got = torch.full((H, W), -1.0, dtype=torch.float32, device="cuda")
-                    ctx.energy_map_device2(frame.data_ptr(), frame.stride(0), W, H, 3, 0, H, a0, a1,
+                    ctx.energy_map_device2(frame.data_ptr(), frame.stride(0), W, H, bpp, 0, H, a0, a1,
                                            b0, b1, n, 0.3, 0.7, got[a0:].data_ptr(), got.stride(0),
                                            torch.cuda.current_stream().cuda_stream, semantics=sem)
                     torch.cuda.synchronize()
