@@ -972,9 +972,10 @@ __device__ __forceinline__ bool rgb_line_grey(const uint32_t (&wd)[K])
 // boundaries.  Entries are written by one elected lane per slot and read only
 // after the wave's refinement phase, so none is ever seen half-written.
 // Grey layers only: for RGB (keyed by the R bytes of windows whose pixels are
-// all grey) the probe's second load of every miss and the extra registers
-// (2 waves per SIMD instead of 3) cost more than the hits saved -- grey line
-// art stored as RGB +28 %, colour strokes +40 % (profiles/r04/memo_ab.jsonl).
+// all grey) the probe's 56-dword row loads, loaded again for every miss, cost
+// more than the hits save -- with this hash and 3 waves per SIMD: grey line
+// art stored as RGB +7 %, colour strokes +22 %, dots +17 %
+// (profiles/r04/memo_ab.jsonl).
 constexpr int kMemoSlots = 64;
 constexpr int kMemoStride = 17;                        // 16 key dwords + the output's bits
 constexpr uint32_t kMemoEmpty = 0xFFFFFFFFu;           // a NaN: never an output
@@ -1004,7 +1005,7 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
 {
     constexpr int N = 8;
     constexpr int HL = Geo<N, SEM>::HL;
-    constexpr bool kMemo = BPP == 1;                // grey layers (RGB: see below)
+    constexpr bool kMemo = BPP == 1;                // grey layers (RGB: see above)
     const MapParams& p = tp.m;
     const unsigned ndirty = *p.dirty_count;
     const int lane = threadIdx.x;
