@@ -963,7 +963,8 @@ __device__ __forceinline__ bool rgb_line_grey(const uint32_t (&wd)[K])
 // Window memo of the dense N = 8 walk (r04).  Tie-dense frames are regular:
 // their flagged windows repeat (straight strokes, grid lines, flat fills, the
 // same glyph), and a window's refined energy depends only on its bytes.  Each
-// wave keeps the windows it refined in an LDS table -- kMemoSlots entries,
+// wave keeps the windows it refined in an LDS table -- kMemoSlots entries
+// (the sparse walk's window buffers, grown to hold them),
 // direct-mapped on a hash of the key, key = the window's 64 bytes (liblqr /
 // preview grey; RGB: the R bytes of a window whose every pixel has R = G = B,
 // which then fix its luma) and the output's bits -- and answers a flagged pixel
@@ -976,7 +977,14 @@ __device__ __forceinline__ bool rgb_line_grey(const uint32_t (&wd)[K])
 // more than the hits save -- with this hash and 3 waves per SIMD: grey line
 // art stored as RGB +7 %, colour strokes +22 %, dots +17 %
 // (profiles/r04/memo_ab.jsonl).
-constexpr int kMemoSlots = 64;
+// 128 slots (8.7 KB with the queue, the block's LDS 11 KB: 3 waves per SIMD
+// still fit): vs 64 the grid 1.50 -> 1.39 ms, line art 0.269 -> 0.265, dots
+// -7 %; 256 costs occupancy (grid 1.62) (profiles/r04/memo_slots_ab.jsonl)
+#ifndef DCTE_MEMO_SLOTS
+#define DCTE_MEMO_SLOTS 128
+#endif
+constexpr int kMemoSlots = DCTE_MEMO_SLOTS;            // a power of two
+static_assert((kMemoSlots & (kMemoSlots - 1)) == 0 && kMemoSlots >= 64, "memo slots");
 constexpr int kMemoStride = 17;                        // 16 key dwords + the output's bits
 constexpr uint32_t kMemoEmpty = 0xFFFFFFFFu;           // a NaN: never an output
 constexpr int kMemoPend = 128;                         // misses waiting for a full batch (< 64 + 64)
@@ -993,7 +1001,7 @@ __device__ __forceinline__ int memo_slot(const uint32_t (&key)[16])
     h ^= h >> 15;
     h *= 0x2c1b3c6du;
     h ^= h >> 12;
-    return (int)(h >> 26);                             // kMemoSlots = 64
+    return (int)(h >> (32 - __builtin_ctz((unsigned)kMemoSlots)));
 }
 
 // The dense-strip walk of one wave: wave `blk` of `nblk` takes dirty strips
@@ -1666,7 +1674,9 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
     // is read only by the luma conversion (the windows only after it)
     // (no dense band here when the dense strips have a kernel of their own)
     constexpr int RAW_D = kOwn ? 0 : (LR * PDW + 1) / 2, WIN_D = (kGroup ? PPW : 1) * WS;
-    constexpr int RW_D = kOtf ? RAW_D + WIN_D : (RAW_D > WIN_D ? RAW_D : WIN_D);
+    constexpr int RW_D0 = kOtf ? RAW_D + WIN_D : (RAW_D > WIN_D ? RAW_D : WIN_D);
+    constexpr int MEMO_D = N == 8 && kOwn ? (kMemoDwords + 1) / 2 : 0;   // the dense walk's memo (doubles)
+    constexpr int RW_D = RW_D0 > MEMO_D ? RW_D0 : MEMO_D;
     __shared__ __attribute__((aligned(16))) double rw_lds[RW_D];
     uint32_t* const raw = reinterpret_cast<uint32_t*>(rw_lds);
     double (*const win)[WS] = reinterpret_cast<double (*)[WS]>(rw_lds + (kOtf ? RAW_D : 0));
