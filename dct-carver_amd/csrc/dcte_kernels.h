@@ -44,7 +44,7 @@ struct MapParams {
     unsigned* dirty_next;    // zeroed by this launch: the next launch's dirty_count
     // N = 8 (and N = 16 liblqr): the DENSE strips (more than kFixDirect flags)
     // once more, as one flat work list for the dense refinement walks
-    // (fix_dense8_flat, fix_dense16_flat): *dense_ctr = {strips << 32 | entries}
+    // (fix_dense16_flat): *dense_ctr = {strips << 32 | entries}
     // (zero when the launch starts; dense_next zeroed by it), and per dense
     // strip dense_list[slot] = {strip, offset of its first entry in the
     // concatenation} -- the offsets ascend with the slot (one 64-bit atomic

@@ -72,18 +72,22 @@ constexpr unsigned kBufFlags = 0x00020000u;  // gfx9 raw buffer dword3
 
 // refinement (below): strips with at most kFixDirect<N> flagged pixels are
 // "sparse" (dcte_fix_strips gathers their windows directly), the rest dense
+#ifndef DCTE_FIX_DIRECT4
+#define DCTE_FIX_DIRECT4 16u    // N = 4 (lane walk since r04)
+#endif
 #ifndef DCTE_FIX_DIRECT8
 #define DCTE_FIX_DIRECT8 16u    // N = 8: most flagged pixels a strip may hold and still be sparse (128 before: dots +47 %, text +4 %; profiles/r03/fix_direct_ab.jsonl)
 #endif
 // (N = 2, 4 keep r02's 128: their dense strips take the band path of
 // dcte_fix_strips, which that value was tuned for, profiles/r02/fix_direct.jsonl)
 template <int N>
-constexpr unsigned kFixDirect = N == 16 ? 32u : (N == 8 ? (unsigned)DCTE_FIX_DIRECT8 : 128u);
-// dense strips walked by a lane-per-pixel (N = 8, fix_dense8_run) /
+constexpr unsigned kFixDirect = N == 16 ? 32u : (N == 8 ? (unsigned)DCTE_FIX_DIRECT8
+                                                          : (N == 4 ? (unsigned)DCTE_FIX_DIRECT4 : 128u));
+// dense strips walked by a lane-per-pixel (N = 4, 8, fix_dense_lane) /
 // lane-quad-per-pixel (N = 16 liblqr, fix_dense16_flat) walk rather than the
 // band path of dcte_fix_strips
 template <int N, int SEM>
-constexpr bool kDenseOwn = N == 8 || (N == 16 && SEM == kSemLqr);
+constexpr bool kDenseOwn = N == 8 || N == 4 || (N == 16 && SEM == kSemLqr);
 // ... N = 16 from the flat list the map kernel numbers (MapParams::dense_list)
 template <int N, int SEM>
 constexpr bool kDenseFlat = N == 16 && kDenseOwn<N, SEM>;
@@ -960,15 +964,15 @@ __device__ __forceinline__ bool rgb_line_grey(const uint32_t (&wd)[K])
     return acc == 0u;
 }
 
-// Window memo of the dense N = 8 walk (r04).  Tie-dense frames are regular:
+// Window memo of the dense lane walks, N = 4 and 8 (r04).  Tie-dense frames are regular:
 // their flagged windows repeat (straight strokes, grid lines, flat fills, the
 // same glyph), and a window's refined energy depends only on its bytes.  Each
 // wave keeps the windows it refined in an LDS table -- kMemoSlots entries
 // (the sparse walk's window buffers, grown to hold them),
-// direct-mapped on a hash of the key, key = the window's 64 bytes (liblqr /
+// direct-mapped on a hash of the key, key = the window's N^2 bytes (liblqr /
 // preview grey; RGB: the R bytes of a window whose every pixel has R = G = B,
 // which then fix its luma) and the output's bits -- and answers a flagged pixel
-// whose window equals an entry's key in all 64 bytes from the entry.  Misses
+// whose window equals an entry's key in all its bytes from the entry.  Misses
 // queue in LDS and are refined 64 at a time, full waves across strip
 // boundaries.  Entries are written by one elected lane per slot and read only
 // after the wave's refinement phase, so none is ever seen half-written.
@@ -985,34 +989,40 @@ __device__ __forceinline__ bool rgb_line_grey(const uint32_t (&wd)[K])
 #endif
 constexpr int kMemoSlots = DCTE_MEMO_SLOTS;            // a power of two
 static_assert((kMemoSlots & (kMemoSlots - 1)) == 0 && kMemoSlots >= 64, "memo slots");
-constexpr int kMemoStride = 17;                        // 16 key dwords + the output's bits
+template <int N>
+constexpr int kMemoKey = N * N / 4;                    // key dwords (N^2 bytes)
+template <int N>
+constexpr int kMemoStride = kMemoKey<N> + 1;           // key + the output's bits
 constexpr uint32_t kMemoEmpty = 0xFFFFFFFFu;           // a NaN: never an output
 constexpr int kMemoPend = 128;                         // misses waiting for a full batch (< 64 + 64)
-constexpr int kMemoDwords = kMemoSlots * kMemoStride + kMemoPend;
+template <int N>
+constexpr int kMemoDwords = kMemoSlots * kMemoStride<N> + kMemoPend;
 
 // slot of a key: FNV-1a over its dwords, then a murmur finaliser, top bits.
 // (A rotate-xor fold is linear over GF(2) and maps the 0x00 / 0xFF byte
 // patterns of line art onto few slots.)
-__device__ __forceinline__ int memo_slot(const uint32_t (&key)[16])
+template <int KD>
+__device__ __forceinline__ int memo_slot(const uint32_t (&key)[KD])
 {
     uint32_t h = 0x811c9dc5u;
 #pragma unroll
-    for (int j = 0; j < 16; j++) h = (h ^ key[j]) * 0x01000193u;
+    for (int j = 0; j < KD; j++) h = (h ^ key[j]) * 0x01000193u;
     h ^= h >> 15;
     h *= 0x2c1b3c6du;
     h ^= h >> 12;
     return (int)(h >> (32 - __builtin_ctz((unsigned)kMemoSlots)));
 }
 
-// The dense-strip walk of one wave: wave `blk` of `nblk` takes dirty strips
-// blk, blk + nblk, ...; `lut` filled by fill_luma_lut; `memo` the wave's
-// kMemoDwords of LDS.
-template <int BPP, int SEM>
-__device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const double* lut, uint32_t* memo,
+// The dense-strip walk of one wave, N = 4 or 8: wave `blk` of `nblk` takes
+// dirty strips blk, blk + nblk, ...; `lut` filled by fill_luma_lut; `memo`
+// the wave's kMemoDwords<N> of LDS.
+template <int N, int BPP, int SEM>
+__device__ __forceinline__ void fix_dense_lane(const TileFixParams& tp, const double* lut, uint32_t* memo,
                                                unsigned blk, unsigned nblk)
 {
-    constexpr int N = 8;
+    static_assert(N == 4 || N == 8, "lane walk: N = 4, 8");
     constexpr int HL = Geo<N, SEM>::HL;
+    constexpr int KD = kMemoKey<N>, MS = kMemoStride<N>, KW = N / 4;   // key dwords, entry, per row
     constexpr bool kMemo = BPP == 1;                // grey layers (RGB: see above)
     const MapParams& p = tp.m;
     const unsigned ndirty = *p.dirty_count;
@@ -1034,24 +1044,24 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
         }
     };
     const unsigned spt = (unsigned)tp.tile_w / 64u;   // strips per map tile
-    constexpr int NW = (8 * BPP + 3) / 4 + 1;         // dwords of a row's 8 pixels, any alignment
-    uint32_t* const pend = memo + kMemoSlots * kMemoStride;
+    constexpr int NW = (N * BPP + 3) / 4 + 1;         // dwords of a row's N pixels, any alignment
+    uint32_t* const pend = memo + kMemoSlots * MS;
     if constexpr (kMemo) {
-        for (int s = lane; s < kMemoSlots; s += 64) memo[s * kMemoStride + 16] = kMemoEmpty;
+        for (int s = lane; s < kMemoSlots; s += 64) memo[s * MS + KD] = kMemoEmpty;
         wave_sync_lds();
     }
 
-    // the window's eight image rows as whole dwords (fast: unclamped and
-    // inside the buffer; otherwise the loads return zeros)
-    auto load_rows = [&](bool active, int x, int y, uint32_t (&fv)[8][NW], uint32_t (&foff)[8], bool (&fast)[8]) {
+    // the window's N image rows as whole dwords (fast: unclamped and inside
+    // the buffer; otherwise the loads return zeros)
+    auto load_rows = [&](bool active, int x, int y, uint32_t (&fv)[N][NW], uint32_t (&foff)[N], bool (&fast)[N]) {
         const int gx0 = x - HL;
-        const bool inside = active && gx0 >= 0 && gx0 + 8 <= p.w;
+        const bool inside = active && gx0 >= 0 && gx0 + N <= p.w;
 #pragma unroll
-        for (int rr = 0; rr < 8; rr++) {
+        for (int rr = 0; rr < N; rr++) {
             const int gy = clampi(y - HL + rr, 0, p.h - 1);
             const uint32_t s0 = base_off + (uint32_t)((long long)(gy - p.in_row0) * p.rowstride) +
                                 (uint32_t)(gx0 * BPP);
-            fast[rr] = inside && ((s0 + 8 * BPP - 1) | 3u) < nrec;
+            fast[rr] = inside && ((s0 + N * BPP - 1) | 3u) < nrec;
             foff[rr] = s0 & 3u;
             const uint32_t a = fast[rr] ? (s0 & ~3u) : 0x7ffffff0u;   // past num_records: zeros
 #pragma unroll
@@ -1061,26 +1071,28 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
     };
     // the window's memo key; false: it has none (a clamped row, or RGB with a
     // pixel whose channels differ)
-    auto make_key = [&](const uint32_t (&fv)[8][NW], const uint32_t (&foff)[8], const bool (&fast)[8],
-                        uint32_t (&key)[16]) -> bool {
+    auto make_key = [&](const uint32_t (&fv)[N][NW], const uint32_t (&foff)[N], const bool (&fast)[N],
+                        uint32_t (&key)[KD]) -> bool {
         bool ok = true;
 #pragma unroll
-        for (int rr = 0; rr < 8; rr++) {
+        for (int rr = 0; rr < N; rr++) {
             uint32_t wd[NW - 1];
 #pragma unroll
             for (int j = 0; j < NW - 1; j++) wd[j] = __builtin_amdgcn_alignbyte(fv[rr][j + 1], fv[rr][j], foff[rr]);
             ok = ok && fast[rr];
             if constexpr (BPP == 1) {
-                key[2 * rr] = wd[0];
-                key[2 * rr + 1] = wd[1];
-            } else {
-                uint32_t g6[6];
 #pragma unroll
-                for (int j = 0; j < 6; j++) g6[j] = wd[j];
-                ok = ok && rgb_line_grey(g6);
+                for (int j = 0; j < KW; j++) key[KW * rr + j] = wd[j];
+            } else {
+                uint32_t g[3 * KW];
+#pragma unroll
+                for (int j = 0; j < 3 * KW; j++) g[j] = wd[j];
+                ok = ok && rgb_line_grey(g);
                 auto byte = [&](int b) { return (wd[b >> 2] >> (8 * (b & 3))) & 255u; };
-                key[2 * rr] = byte(0) | byte(3) << 8 | byte(6) << 16 | byte(9) << 24;
-                key[2 * rr + 1] = byte(12) | byte(15) << 8 | byte(18) << 16 | byte(21) << 24;
+#pragma unroll
+                for (int j = 0; j < KW; j++)
+                    key[KW * rr + j] = byte(12 * j) | byte(12 * j + 3) << 8 | byte(12 * j + 6) << 16 |
+                                       byte(12 * j + 9) << 24;
             }
         }
         return ok;
@@ -1089,22 +1101,22 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
     // refine the pixel of each active lane from its loaded rows (fp64, the
     // reference's order) and, with `ins` (uniform), enter its window into the
     // memo
-    auto refine_rows = [&](bool active, int x, int y, const uint32_t (&fv)[8][NW], const uint32_t (&foff)[8],
-                           const bool (&fast)[8], bool ins) {
+    auto refine_rows = [&](bool active, int x, int y, const uint32_t (&fv)[N][NW], const uint32_t (&foff)[N],
+                           const bool (&fast)[N], bool ins) {
         if (!active) return;
         int slot = -1;                                   // the memo slot this lane fills
         if (kMemo && ins) {
-            uint32_t key[16];
+            uint32_t key[KD];
             const bool keyed = make_key(fv, foff, fast, key);
             int s = 0;
             if (keyed) {
                 s = memo_slot(key);
-                memo[s * kMemoStride + 16] = (uint32_t)lane;        // one lane per slot wins
+                memo[s * MS + KD] = (uint32_t)lane;                 // one lane per slot wins
             }
             wave_sync_lds();
-            if (keyed && memo[s * kMemoStride + 16] == (uint32_t)lane) {
+            if (keyed && memo[s * MS + KD] == (uint32_t)lane) {
 #pragma unroll
-                for (int j = 0; j < 16; j++) memo[s * kMemoStride + j] = key[j];
+                for (int j = 0; j < KD; j++) memo[s * MS + j] = key[j];
                 slot = s;                                // its value follows the refinement
             }
         }
@@ -1116,19 +1128,19 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
         if constexpr (SEM == kSemLqr && BPP == 3) {
             bool mine = true;
 #pragma unroll
-            for (int rr = 0; rr < 8; rr++) {
-                uint32_t wd[6];
+            for (int rr = 0; rr < N; rr++) {
+                uint32_t wd[3 * KW];
 #pragma unroll
-                for (int j = 0; j < 6; j++) wd[j] = __builtin_amdgcn_alignbyte(fv[rr][j + 1], fv[rr][j], foff[rr]);
+                for (int j = 0; j < 3 * KW; j++) wd[j] = __builtin_amdgcn_alignbyte(fv[rr][j + 1], fv[rr][j], foff[rr]);
                 mine = mine && fast[rr] && rgb_line_grey(wd);
             }
             grey = __all(mine);                  // uniform
         }
-        double d[64];
+        double d[N * N];
         const int gx0 = x - HL;
 #pragma unroll
-        for (int r = 0; r < 8; r++) {
-            double lv[8];
+        for (int r = 0; r < N; r++) {
+            double lv[N];
             if (fast[r]) {
                 uint32_t wd[NW - 1];
 #pragma unroll
@@ -1136,10 +1148,10 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
                 auto byte = [&](int b) { return (wd[b >> 2] >> (8 * (b & 3))) & 255u; };
                 if (grey) {
 #pragma unroll
-                    for (int c = 0; c < 8; c++) lv[c] = lut[768 + byte(c * BPP)];
+                    for (int c = 0; c < N; c++) lv[c] = lut[768 + byte(c * BPP)];
                 } else {
 #pragma unroll
-                    for (int c = 0; c < 8; c++)
+                    for (int c = 0; c < N; c++)
                         lv[c] = luma3(byte(c * BPP), BPP > 1 ? byte(c * BPP + 1) : 0u, BPP > 1 ? byte(c * BPP + 2) : 0u);
                 }
             } else {
@@ -1148,21 +1160,21 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
                 const int gy = clampi(y - HL + r, 0, p.h - 1);
                 const uint8_t* row = p.px + (long long)(gy - p.in_row0) * p.rowstride;
 #pragma unroll
-                for (int c = 0; c < 8; c++) {
+                for (int c = 0; c < N; c++) {
                     const uint8_t* q8 = row + (long long)clampi(gx0 + c, 0, p.w - 1) * BPP;
                     lv[c] = luma3(q8[0], BPP > 1 ? q8[1] : 0u, BPP > 1 ? q8[2] : 0u);
                 }
             }
             // image row r, pixel c: liblqr data[c][r], preview data[r][c]
 #pragma unroll
-            for (int c = 0; c < 8; c++) d[SEM == kSemLqr ? c * 8 + r : r * 8 + c] = lv[c];
+            for (int c = 0; c < N; c++) d[SEM == kSemLqr ? c * N + r : r * N + c] = lv[c];
         }
         double m;
         bool edge;
-        refine_regs<8>(d, tp.ct, m, edge);
+        refine_regs<N>(d, tp.ct, m, edge);
         const float v = edge ? (float)(m * (double)p.edges) : (float)(m * (double)p.textures);
         p.out[(long long)(y - p.y0) * p.out_stride + x] = v;
-        if (kMemo && slot >= 0) memo[slot * kMemoStride + 16] = __float_as_uint(v);
+        if (kMemo && slot >= 0) memo[slot * MS + KD] = __float_as_uint(v);
     };
 
     // (without the memo, the direct walk: queueing RGB entries for full
@@ -1183,9 +1195,9 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
                 if (q >= cnt) continue;
                 const unsigned loc = list[q];
                 const int x = sx0 + (int)(loc & 63), y = ys + (int)(loc >> 6);
-                uint32_t fv[8][NW];
-                uint32_t foff[8];
-                bool fast[8];
+                uint32_t fv[N][NW];
+                uint32_t foff[N];
+                bool fast[N];
                 load_rows(true, x, y, fv, foff, fast);
                 refine_rows(true, x, y, fv, foff, fast, false);
             }
@@ -1229,17 +1241,17 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
             const int x = sx0 + (int)(loc & 63), y = ys + (int)(loc >> 6);
             bool hit = false;
             if (use) {
-                uint32_t fv[8][NW];
-                uint32_t foff[8];
-                bool fast[8];
+                uint32_t fv[N][NW];
+                uint32_t foff[N];
+                bool fast[N];
                 load_rows(act, x, y, fv, foff, fast);
-                uint32_t key[16];
+                uint32_t key[KD];
                 if (act && make_key(fv, foff, fast, key)) {
-                    const uint32_t* ent = memo + memo_slot(key) * kMemoStride;
-                    const uint32_t val = ent[16];
+                    const uint32_t* ent = memo + memo_slot(key) * MS;
+                    const uint32_t val = ent[KD];
                     uint32_t diff = val == kMemoEmpty ? 1u : 0u;
 #pragma unroll
-                    for (int j = 0; j < 16; j++) diff |= ent[j] ^ key[j];
+                    for (int j = 0; j < KD; j++) diff |= ent[j] ^ key[j];
                     if (diff == 0u) {
                         p.out[(long long)(y - p.y0) * p.out_stride + x] = __uint_as_float(val);
                         hit = true;
@@ -1278,9 +1290,9 @@ __device__ __forceinline__ void fix_dense8_run(const TileFixParams& tp, const do
             if ((unsigned long long)yr * uw > e) yr--;     // the quotient rounded up
             const int x = (int)(e - yr * uw), y = p.y0 + (int)yr;
             if (act) {
-                uint32_t fv[8][NW];
-                uint32_t foff[8];
-                bool fast[8];
+                uint32_t fv[N][NW];
+                uint32_t foff[N];
+                bool fast[N];
                 load_rows(true, x, y, fv, foff, fast);
                 refine_rows(true, x, y, fv, foff, fast, use);
             }
@@ -1657,9 +1669,9 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
     // weighted quotients k_c (v / 255) tabulated so a luma is two fp64 adds
     // ((k_r r + k_g g) + k_b b, the reference's order): line art RGB 1.41 ->
     // 1.33 ms; at N = 16 the same costs +30 % (profiles/r02/fix_otf_ab.jsonl)
-    constexpr bool kTab = SEM == kSemLqr && BPP == 3 && N == 8;
+    constexpr bool kTab = SEM == kSemLqr && BPP == 3 && (N == 8 || N == 4);
     constexpr bool kOtf = BPP == 1 || kTab;
-    // dense strips go to fix_dense8_run / fix_dense16_flat (kDenseOwn): no band
+    // dense strips go to fix_dense_lane / fix_dense16_flat (kDenseOwn): no band
     // staging here, and the N = 16 RGB dense blocks want pre-weighted tables
     constexpr bool kOwn = kDenseOwn<N, SEM>;
     constexpr bool kTab16 = N == 16 && kOwn && BPP == 3;
@@ -1675,7 +1687,7 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
     // (no dense band here when the dense strips have a kernel of their own)
     constexpr int RAW_D = kOwn ? 0 : (LR * PDW + 1) / 2, WIN_D = (kGroup ? PPW : 1) * WS;
     constexpr int RW_D0 = kOtf ? RAW_D + WIN_D : (RAW_D > WIN_D ? RAW_D : WIN_D);
-    constexpr int MEMO_D = N == 8 && kOwn ? (kMemoDwords + 1) / 2 : 0;   // the dense walk's memo (doubles)
+    constexpr int MEMO_D = N <= 8 && kOwn && BPP == 1 ? (kMemoDwords<N> + 1) / 2 : 0;   // the lane walk's memo (grey)
     constexpr int RW_D = RW_D0 > MEMO_D ? RW_D0 : MEMO_D;
     __shared__ __attribute__((aligned(16))) double rw_lds[RW_D];
     uint32_t* const raw = reinterpret_cast<uint32_t*>(rw_lds);
@@ -1687,13 +1699,13 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
         if (blockIdx.x >= (unsigned)tp.sparse_blocks) {
             const unsigned blk = blockIdx.x - (unsigned)tp.sparse_blocks;
             const unsigned nblk = gridDim.x - (unsigned)tp.sparse_blocks;
-            if constexpr (N == 8) {
+            if constexpr (N <= 8) {
                 if (blk >= ndirty) return;             // uniform
                 fill_luma_lut<kTab>(lut, threadIdx.x);
                 wave_sync_lds();
                 // the window buffers of the sparse walk hold the dense walk's memo
-                static_assert(sizeof(rw_lds) >= kMemoDwords * sizeof(uint32_t), "memo fits");
-                fix_dense8_run<BPP, SEM>(tp, lut, reinterpret_cast<uint32_t*>(rw_lds), blk, nblk);
+                static_assert(BPP != 1 || sizeof(rw_lds) >= kMemoDwords<N> * sizeof(uint32_t), "memo fits");
+                fix_dense_lane<N, BPP, SEM>(tp, lut, reinterpret_cast<uint32_t*>(rw_lds), blk, nblk);
             } else {
                 fill_luma_lut<kTab16>(lut, threadIdx.x);
                 wave_sync_lds();
@@ -2301,7 +2313,7 @@ static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
         const long long most = kDenseFlat<N, SEM>
                                    ? ((long long)nstrips * 64 * p.m.tile_h + kDenseBatch16 - 1) / kDenseBatch16
                                    : nstrips;
-        const long long dmax = (long long)resident * (N == 8 && BPP == 1 ? DCTE_DENSE_OVERSUB_MEMO : DCTE_DENSE_OVERSUB);
+        const long long dmax = (long long)resident * (N <= 8 && BPP == 1 ? DCTE_DENSE_OVERSUB_MEMO : DCTE_DENSE_OVERSUB);
         const int dblocks = (int)(most < dmax ? most : dmax);
         TileFixParams q = p;
         q.sparse_blocks = blocks;
