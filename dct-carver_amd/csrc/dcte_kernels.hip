@@ -1069,16 +1069,21 @@ __device__ __forceinline__ void fix_dense_lane(const TileFixParams& tp, const do
                 fv[rr][j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(a + 4u * j), 0, 0);
         }
     };
+    // the rows' bytes from their first pixel on (aligned once: the raw dwords
+    // die here)
+    auto align_rows = [&](const uint32_t (&fv)[N][NW], const uint32_t (&foff)[N], uint32_t (&wa)[N][NW - 1]) {
+#pragma unroll
+        for (int rr = 0; rr < N; rr++)
+#pragma unroll
+            for (int j = 0; j < NW - 1; j++) wa[rr][j] = __builtin_amdgcn_alignbyte(fv[rr][j + 1], fv[rr][j], foff[rr]);
+    };
     // the window's memo key; false: it has none (a clamped row, or RGB with a
     // pixel whose channels differ)
-    auto make_key = [&](const uint32_t (&fv)[N][NW], const uint32_t (&foff)[N], const bool (&fast)[N],
-                        uint32_t (&key)[KD]) -> bool {
+    auto make_key = [&](const uint32_t (&wa)[N][NW - 1], const bool (&fast)[N], uint32_t (&key)[KD]) -> bool {
         bool ok = true;
 #pragma unroll
         for (int rr = 0; rr < N; rr++) {
-            uint32_t wd[NW - 1];
-#pragma unroll
-            for (int j = 0; j < NW - 1; j++) wd[j] = __builtin_amdgcn_alignbyte(fv[rr][j + 1], fv[rr][j], foff[rr]);
+            const uint32_t (&wd)[NW - 1] = wa[rr];
             ok = ok && fast[rr];
             if constexpr (BPP == 1) {
 #pragma unroll
@@ -1101,13 +1106,13 @@ __device__ __forceinline__ void fix_dense_lane(const TileFixParams& tp, const do
     // refine the pixel of each active lane from its loaded rows (fp64, the
     // reference's order) and, with `ins` (uniform), enter its window into the
     // memo
-    auto refine_rows = [&](bool active, int x, int y, const uint32_t (&fv)[N][NW], const uint32_t (&foff)[N],
-                           const bool (&fast)[N], bool ins) {
+    auto refine_rows = [&](bool active, int x, int y, const uint32_t (&wa)[N][NW - 1], const bool (&fast)[N],
+                           bool ins) {
         if (!active) return;
         int slot = -1;                                   // the memo slot this lane fills
         if (kMemo && ins) {
             uint32_t key[KD];
-            const bool keyed = make_key(fv, foff, fast, key);
+            const bool keyed = make_key(wa, fast, key);
             int s = 0;
             if (keyed) {
                 s = memo_slot(key);
@@ -1131,7 +1136,7 @@ __device__ __forceinline__ void fix_dense_lane(const TileFixParams& tp, const do
             for (int rr = 0; rr < N; rr++) {
                 uint32_t wd[3 * KW];
 #pragma unroll
-                for (int j = 0; j < 3 * KW; j++) wd[j] = __builtin_amdgcn_alignbyte(fv[rr][j + 1], fv[rr][j], foff[rr]);
+                for (int j = 0; j < 3 * KW; j++) wd[j] = wa[rr][j];
                 mine = mine && fast[rr] && rgb_line_grey(wd);
             }
             grey = __all(mine);                  // uniform
@@ -1142,9 +1147,7 @@ __device__ __forceinline__ void fix_dense_lane(const TileFixParams& tp, const do
         for (int r = 0; r < N; r++) {
             double lv[N];
             if (fast[r]) {
-                uint32_t wd[NW - 1];
-#pragma unroll
-                for (int j = 0; j < NW - 1; j++) wd[j] = __builtin_amdgcn_alignbyte(fv[r][j + 1], fv[r][j], foff[r]);
+                const uint32_t (&wd)[NW - 1] = wa[r];
                 auto byte = [&](int b) { return (wd[b >> 2] >> (8 * (b & 3))) & 255u; };
                 if (grey) {
 #pragma unroll
@@ -1199,7 +1202,9 @@ __device__ __forceinline__ void fix_dense_lane(const TileFixParams& tp, const do
                 uint32_t foff[N];
                 bool fast[N];
                 load_rows(true, x, y, fv, foff, fast);
-                refine_rows(true, x, y, fv, foff, fast, false);
+                uint32_t wa[N][NW - 1];
+                align_rows(fv, foff, wa);
+                refine_rows(true, x, y, wa, fast, false);
             }
         }
         return;
@@ -1245,8 +1250,10 @@ __device__ __forceinline__ void fix_dense_lane(const TileFixParams& tp, const do
                 uint32_t foff[N];
                 bool fast[N];
                 load_rows(act, x, y, fv, foff, fast);
+                uint32_t wa[N][NW - 1];
+                align_rows(fv, foff, wa);
                 uint32_t key[KD];
-                if (act && make_key(fv, foff, fast, key)) {
+                if (act && make_key(wa, fast, key)) {
                     const uint32_t* ent = memo + memo_slot(key) * MS;
                     const uint32_t val = ent[KD];
                     uint32_t diff = val == kMemoEmpty ? 1u : 0u;
@@ -1294,7 +1301,9 @@ __device__ __forceinline__ void fix_dense_lane(const TileFixParams& tp, const do
                 uint32_t foff[N];
                 bool fast[N];
                 load_rows(true, x, y, fv, foff, fast);
-                refine_rows(true, x, y, fv, foff, fast, use);
+                uint32_t wa[N][NW - 1];
+                align_rows(fv, foff, wa);
+                refine_rows(true, x, y, wa, fast, use);
             }
             wave_sync_lds();
         }
