@@ -350,6 +350,30 @@ def test_tie_dense_one_launch(ctx):
         torch.cuda.empty_cache()
 
 
+def test_tie_dense_full_size_n4(ctx):
+    """N = 4 on the frames whose ties it refines most (the lane walk with the
+    grey memo since r04): line art as RGB (5.5 % flagged) and grey dots on
+    flat ground (10 %) at 8192^2, each in one device launch -- every pixel
+    against the oracle, 0 class flips."""
+    torch = _torch()
+    S = 8192
+    yy, xx = np.ogrid[0:S, 0:S]
+    ink = (yy % 23 == 0) | (xx % 31 == 0) | ((xx + 2 * yy) % 97 == 0)
+    line = np.repeat(np.where(ink, 0, 255).astype(np.uint8)[..., None], 3, -1)
+    del ink
+    dots = np.where(np.random.default_rng(22).random((S, S), dtype=np.float32) < 1 / 64,
+                    255, 16).astype(np.uint8)
+    for name, img in (("lineart_rgb", line), ("dots_grey", dots)):
+        out = torch.empty((S, S), dtype=torch.float32, device="cuda")
+        ctx.energy_map_tensor(torch.from_numpy(img).cuda(), out, 4, 0.3, 0.7)
+        torch.cuda.synchronize()
+        ref = O.energy_map(img, 4, 0.3, 0.7, nthreads=NTHREADS)
+        st = _compare_full(out, ref, 0.3, 0.7, f"{name} {S}^2 N=4 one launch")
+        print(name, "N=4", st)
+        del out, ref
+        torch.cuda.empty_cache()
+
+
 def test_tie_dense_full_size_n16(ctx):
     """N = 16 (configs[4]'s block size, 8192^2) on line art: 4.3 % of the
     pixels flagged, their dense strips refined four lanes per pixel with the
@@ -578,7 +602,7 @@ def test_energy_windows_bit_exact(ctx, n):
         assert np.array_equal(got, ref), n
 
 
-@pytest.mark.parametrize("n", [8, 16])
+@pytest.mark.parametrize("n", [4, 8, 16])
 def test_grey_rgb_refinement_paths(n):
     """The dense refinement walks read liblqr RGB luma through one table when
     every pixel of a batch's windows is grey (R = G = B) and through three
@@ -610,7 +634,7 @@ def test_grey_rgb_refinement_paths(n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [8, 16])
+@pytest.mark.parametrize("n", [4, 8, 16])
 def test_window_memo_near_duplicates(n):
     """The dense walks answer a window whose bytes equal an earlier refined
     window's from a per-wave memo.  Frames built to defeat a wrong key: strokes
