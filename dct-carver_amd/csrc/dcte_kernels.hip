@@ -947,6 +947,23 @@ __device__ __forceinline__ void fill_luma_lut(double* lut, int lane)
     }
 }
 
+// Preview RGB / RGBA (the lane walks): RGB2LUMINANCE (src/render.h:5, preview_
+// in dcte_luma.h) is ((16 + 0.2568 r) + 0.5041 g) + 0.0979 b in double, then
+// truncated to u8: the three terms tabulated as computed (no contraction), so
+// (lut[r] + lut[256 + g]) + lut[512 + b] is the same double; lut[768 + v] is
+// the u8 luma of the grey pixel (v, v, v)
+__device__ __forceinline__ void fill_preview_lut(double* lut, int lane)
+{
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const int v = lane + 64 * t;
+        lut[v] = 16.0 + v * 0.2568;
+        lut[256 + v] = v * 0.5041;
+        lut[512 + v] = v * 0.0979;
+        lut[768 + v] = (double)preview_luma((unsigned)v, (unsigned)v, (unsigned)v, 3);
+    }
+}
+
 // RGB bytes of a window line (8 pixels in 6 dwords, wd): every pixel grey
 // (R = G = B)?  d = the stream XOR itself shifted by one byte; within each
 // pixel's three bytes the first two of d are zero iff the channels agree.
@@ -1035,10 +1052,13 @@ __device__ __forceinline__ void fix_dense_lane(const TileFixParams& tp, const do
         reinterpret_cast<void*>(pbase - base_off), (short)0, (int)nrec, (int)kBufFlags);
     // liblqr luma (src/render.c:315, LQR_ER_LUMA) [liblqr, unverified] in the
     // reference's order ((k_r r + k_g g) + k_b b); preview: RGB2LUMINANCE
+    // (colour layers through the per-channel tables of fill_preview_lut)
     auto luma3 = [&](uint32_t c0, uint32_t c1, uint32_t c2) -> double {
         if constexpr (SEM == kSemLqr) {
             if constexpr (BPP == 1) return lut[c0];
             else return lut[c0] + lut[256 + c1] + lut[512 + c2];
+        } else if constexpr (BPP >= 3) {
+            return (double)(unsigned char)((lut[c0] + lut[256 + c1]) + lut[512 + c2]);
         } else {
             return (double)preview_luma(c0, c1, c2, BPP);
         }
@@ -1125,12 +1145,12 @@ __device__ __forceinline__ void fix_dense_lane(const TileFixParams& tp, const do
                 slot = s;                                // its value follows the refinement
             }
         }
-        // liblqr RGB: when every window pixel of every lane is grey (scanned
+        // RGB: when every window pixel of every lane is grey (scanned
         // documents, line art stored as RGB), one table read per element
-        // (lut[768 + v], the same double the three reads and two adds give)
-        // instead of three
+        // (lut[768 + v], the same double the three reads and two adds give --
+        // liblqr -- or the same u8 luma -- preview) instead of three
         bool grey = false;
-        if constexpr (SEM == kSemLqr && BPP == 3) {
+        if constexpr (BPP == 3) {
             bool mine = true;
 #pragma unroll
             for (int rr = 0; rr < N; rr++) {
@@ -1684,7 +1704,8 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
     // staging here, and the N = 16 RGB dense blocks want pre-weighted tables
     constexpr bool kOwn = kDenseOwn<N, SEM>;
     constexpr bool kTab16 = N == 16 && kOwn && BPP == 3;
-    __shared__ double lut[(kTab || kTab16) ? 4 * 256 : 256];
+    constexpr bool kTabP = SEM == kSemPreview && N <= 8 && kOwn && BPP >= 3;   // fill_preview_lut
+    __shared__ double lut[(kTab || kTab16 || kTabP) ? 4 * 256 : 256];
     __shared__ double lum[(kOtf || kOwn) ? 1 : LR * LW];   // fp64 luma of one band (+ halo), needed columns
     __shared__ unsigned char mis[LR];                  // byte offset of each raw row's first pixel
     __shared__ unsigned char colidx[(kOtf || kOwn) ? 1 : LW];   // the needed luma columns, ascending
@@ -1710,7 +1731,8 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
             const unsigned nblk = gridDim.x - (unsigned)tp.sparse_blocks;
             if constexpr (N <= 8) {
                 if (blk >= ndirty) return;             // uniform
-                fill_luma_lut<kTab>(lut, threadIdx.x);
+                if constexpr (kTabP) fill_preview_lut(lut, threadIdx.x);
+                else fill_luma_lut<kTab>(lut, threadIdx.x);
                 wave_sync_lds();
                 // the window buffers of the sparse walk hold the dense walk's memo
                 static_assert(BPP != 1 || sizeof(rw_lds) >= kMemoDwords<N> * sizeof(uint32_t), "memo fits");

@@ -62,6 +62,7 @@ def main():
     ap.add_argument("--frames", default="", help="comma-separated frame-name prefixes (default: all)")
     ap.add_argument("--tau", type=float, default=4e-6,
                     help="tie_tau of the timed calls (1 = every pixel refined: the exact mode)")
+    ap.add_argument("--preview", action="store_true", help="preview semantics (default: liblqr)")
     a = ap.parse_args()
     if a.lib:
         os.environ["DCTE_LIB"] = os.path.abspath(a.lib)
@@ -69,6 +70,7 @@ def main():
     import dctenergy
     dev = torch.device("cuda", 0)
     S, n, e, t = a.size, a.n, a.edges, a.textures
+    sem = dctenergy.DCTE_PREVIEW if a.preview else dctenergy.DCTE_LQR
     out = torch.empty((S, S), dtype=torch.float32, device=dev)
     with dctenergy.Context(ngpus=1) as ctx:
         for name, fr in frames(S, torch, dev).items():
@@ -79,14 +81,14 @@ def main():
             def timed(tau):
                 """-> (stream ms per call, map-launch ms per call)"""
                 ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, tau)
-                ctx.energy_map_tensor(fr, out, n, e, t)        # warm
+                ctx.energy_map_tensor(fr, out, n, e, t, semantics=sem)        # warm
                 torch.cuda.synchronize()
                 ctx.profile_read()
                 ctx.set_option(dctenergy.DCTE_OPT_PROFILE, 1)
                 a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a0.record(stream)
                 for _ in range(a.iters):
-                    ctx.energy_map_tensor(fr, out, n, e, t)
+                    ctx.energy_map_tensor(fr, out, n, e, t, semantics=sem)
                 a1.record(stream)
                 torch.cuda.synchronize()
                 ctx.set_option(dctenergy.DCTE_OPT_PROFILE, 0)
@@ -107,10 +109,10 @@ def main():
             ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, a.tau)
             # flagged count: the host entry point reports it (same kernels)
             host = fr.cpu().numpy()
-            ctx.energy_map(host, n, e, t)
+            ctx.energy_map(host, n, e, t, semantics=sem)
             flagged = ctx.last_refined
             del host
-            res = {"frame": name, "size": S, "n": n, "tau": a.tau, "lib": os.path.basename(dctenergy.LIB_PATH),
+            res = {"frame": name, "size": S, "n": n, "semantics": "preview" if a.preview else "liblqr", "tau": a.tau, "lib": os.path.basename(dctenergy.LIB_PATH),
                    "flagged": flagged,
                    "flagged_frac": round(flagged / (S * S), 5),
                    "map_ms": round(ms_map, 4), "map_plus_fix_ms": round(ms_all, 4),
