@@ -87,7 +87,7 @@ constexpr unsigned kFixDirect = N == 16 ? 32u : (N == 8 ? (unsigned)DCTE_FIX_DIR
 // lane-quad-per-pixel (N = 16 liblqr, fix_dense16_flat) walk rather than the
 // band path of dcte_fix_strips
 template <int N, int SEM>
-constexpr bool kDenseOwn = N == 8 || N == 4 || (N == 16 && SEM == kSemLqr);
+constexpr bool kDenseOwn = N == 8 || N == 4 || N == 16;
 // ... N = 16 from the flat list the map kernel numbers (MapParams::dense_list)
 template <int N, int SEM>
 constexpr bool kDenseFlat = N == 16 && kDenseOwn<N, SEM>;
@@ -1488,12 +1488,12 @@ struct D16Rows {
     bool valid;
 };
 
-template <int BPP>
+template <int BPP, int SEM>
 __device__ __forceinline__ void fix_dense16_flat(const TileFixParams& tp, const double* lut,
                                                  unsigned blk, unsigned nblk)
 {
     constexpr int N = 16;
-    constexpr int HL = Geo<N, kSemLqr>::HL;
+    constexpr int HL = Geo<N, SEM>::HL;
     constexpr int NW = D16Rows<BPP>::NW;
     const MapParams& p = tp.m;
     DenseWalk<16> dw;
@@ -1507,10 +1507,17 @@ __device__ __forceinline__ void fix_dense16_flat(const TileFixParams& tp, const 
     __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<void*>(pbase - base_off), (short)0, (int)nrec, (int)kBufFlags);
     // liblqr luma (src/render.c:315, LQR_ER_LUMA) [liblqr, unverified]:
-    // grey v / 255; RGB (k_r r + k_g g) + k_b b through the pre-weighted tables
+    // grey v / 255; RGB (k_r r + k_g g) + k_b b through the pre-weighted tables.
+    // Preview: RGB2LUMINANCE (colour through fill_preview_lut's tables)
     auto luma3 = [&](uint32_t c0, uint32_t c1, uint32_t c2) -> double {
-        if constexpr (BPP == 1) return lut[c0];
-        else return lut[c0] + lut[256 + c1] + lut[512 + c2];
+        if constexpr (SEM == kSemLqr) {
+            if constexpr (BPP == 1) return lut[c0];
+            else return lut[c0] + lut[256 + c1] + lut[512 + c2];
+        } else if constexpr (BPP >= 3) {
+            return (double)(unsigned char)((lut[c0] + lut[256 + c1]) + lut[512 + c2]);
+        } else {
+            return (double)preview_luma(c0, c1, c2, BPP);
+        }
     };
     // this lane's four lines: image rows y - HL + 4q + jj, pixels x - HL .. x - HL + 15
     auto row_stage = [&](unsigned loc, int sx0, int ys, bool valid, D16Rows<BPP>& R) {
@@ -1626,27 +1633,9 @@ __device__ __forceinline__ void fix_dense16_flat(const TileFixParams& tp, const 
             row_stage(locN, sxN, ysN, vN, R);
             if (dw.next(bn) < nb) list16(dw.next(bn), locN, sxN, ysN, vN);
         }
-        // first pass: the lane's four lines along the first index
-#pragma unroll
-        for (int jj = 0; jj < 4; jj++) {
-            double line[16];
-#pragma unroll
-            for (int c = 0; c < 16; c++) line[c] = X[c >> 2][c & 3][jj];
-            r64::step16(line, 1);
-#pragma unroll
-            for (int c = 0; c < 16; c++) X[c >> 2][c & 3][jj] = line[c];
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        transpose_quad(X);
-        // second pass: coefficient rows k1 = 4q + kk along the second index,
-        // and their maxima for the scan
         double rmax[4], c01 = 0.0, c10 = 0.0, r0_2 = -1.0, r1_1 = -1.0;
-#pragma unroll
-        for (int kk = 0; kk < 4; kk++) {
-            double line[16];
-#pragma unroll
-            for (int j = 0; j < 16; j++) line[j] = X[j >> 2][kk][j & 3];
-            r64::step16(line, 1);
+        // the maxima of coefficient row k1 = 4q + kk after its second pass
+        auto row_max = [&](int kk, const double (&line)[16]) {
             double m2 = -1.0;
 #pragma unroll
             for (int k2 = 2; k2 < 16; k2++) m2 = fmax(m2, fabs(line[k2]));
@@ -1658,7 +1647,56 @@ __device__ __forceinline__ void fix_dense16_flat(const TileFixParams& tp, const 
                 r1_1 = fmax(m2, fabs(line[1]));
             }
             rmax[kk] = fmax(fmax(fabs(line[0]), fabs(line[1])), m2);
-            __builtin_amdgcn_sched_barrier(0);
+        };
+        if constexpr (SEM == kSemLqr) {
+            // first pass: the lane's four lines along the first index (x)
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++) {
+                double line[16];
+#pragma unroll
+                for (int c = 0; c < 16; c++) line[c] = X[c >> 2][c & 3][jj];
+                r64::step16(line, 1);
+#pragma unroll
+                for (int c = 0; c < 16; c++) X[c >> 2][c & 3][jj] = line[c];
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            transpose_quad(X);
+            // second pass: coefficient rows k1 = 4q + kk along the second index
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) {
+                double line[16];
+#pragma unroll
+                for (int j = 0; j < 16; j++) line[j] = X[j >> 2][kk][j & 3];
+                r64::step16(line, 1);
+                row_max(kk, line);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+            // preview data[r][c]: the first index is the image row, so the
+            // lane first takes pixels 4q .. 4q + 3 with all 16 rows (the same
+            // exchange), runs the first pass down them, and the exchange back
+            // leaves it first-pass rows k1 = 4q + jj across all pixels
+            transpose_quad(X);
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) {
+                double line[16];
+#pragma unroll
+                for (int l = 0; l < 16; l++) line[l] = X[l >> 2][kk][l & 3];
+                r64::step16(line, 1);
+#pragma unroll
+                for (int l = 0; l < 16; l++) X[l >> 2][kk][l & 3] = line[l];
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            transpose_quad(X);
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++) {
+                double line[16];
+#pragma unroll
+                for (int c = 0; c < 16; c++) line[c] = X[c >> 2][c & 3][jj];
+                r64::step16(line, 1);
+                row_max(jj, line);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
         // indices past N = (1, 0) in the scan order: rows 1 (from k2 = 1), 2, 3 of
         // quarter 0, every row of the others
@@ -1703,8 +1741,8 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
     // dense strips go to fix_dense_lane / fix_dense16_flat (kDenseOwn): no band
     // staging here, and the N = 16 RGB dense blocks want pre-weighted tables
     constexpr bool kOwn = kDenseOwn<N, SEM>;
-    constexpr bool kTab16 = N == 16 && kOwn && BPP == 3;
-    constexpr bool kTabP = SEM == kSemPreview && N <= 8 && kOwn && BPP >= 3;   // fill_preview_lut
+    constexpr bool kTab16 = N == 16 && kOwn && BPP == 3 && SEM == kSemLqr;
+    constexpr bool kTabP = SEM == kSemPreview && kOwn && BPP >= 3;   // fill_preview_lut
     __shared__ double lut[(kTab || kTab16 || kTabP) ? 4 * 256 : 256];
     __shared__ double lum[(kOtf || kOwn) ? 1 : LR * LW];   // fp64 luma of one band (+ halo), needed columns
     __shared__ unsigned char mis[LR];                  // byte offset of each raw row's first pixel
@@ -1738,9 +1776,10 @@ __global__ __launch_bounds__(64, (kFixMinWaves<N, BPP>)) void dcte_fix_strips(co
                 static_assert(BPP != 1 || sizeof(rw_lds) >= kMemoDwords<N> * sizeof(uint32_t), "memo fits");
                 fix_dense_lane<N, BPP, SEM>(tp, lut, reinterpret_cast<uint32_t*>(rw_lds), blk, nblk);
             } else {
-                fill_luma_lut<kTab16>(lut, threadIdx.x);
+                if constexpr (kTabP) fill_preview_lut(lut, threadIdx.x);
+                else fill_luma_lut<kTab16>(lut, threadIdx.x);
                 wave_sync_lds();
-                fix_dense16_flat<BPP>(tp, lut, blk, nblk);
+                fix_dense16_flat<BPP, SEM>(tp, lut, blk, nblk);
             }
             return;
         }
@@ -2383,7 +2422,7 @@ hipError_t launch_fix_tiles(int n, int bpp, int sem, const TileFixParams& p, hip
 
 int dense_batch_entries(int n, int sem)
 {
-    if (n == 16 && sem == kSemLqr) return kDenseFlat<16, kSemLqr> ? (int)kDenseBatch16 : 0;
+    if (n == 16) return (sem == kSemLqr ? kDenseFlat<16, kSemLqr> : kDenseFlat<16, kSemPreview>) ? (int)kDenseBatch16 : 0;
     return 0;
 }
 
