@@ -2371,7 +2371,11 @@ static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
             resident = 2048;
         if (dev >= 0 && dev < kMaxDevices) cache[dev].store(resident, std::memory_order_relaxed);
     }
-    const int blocks = nstrips < resident ? nstrips : resident;
+    // the sparse walk takes SB strips per block and pass (dcte_fix_strips):
+    // more blocks than batches only launch to exit (a band's edge ranges)
+    constexpr int SB = N >= 8 ? 64 / N : 8;            // = dcte_fix_strips' SB
+    const int batches = (nstrips + SB - 1) / SB;
+    const int blocks = batches < resident ? batches : resident;
     if constexpr (kDenseFlat<N, SEM>) {
         // the flat list's batch map first (one wave per possible listed strip)
         hipLaunchKernelGGL((dcte_dense_index<kDenseBatch16>), dim3((nstrips + 3) / 4), dim3(256), 0, s, p);
