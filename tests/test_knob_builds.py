@@ -30,6 +30,7 @@ KNOBS = {
     "DCTE_TSTAMP": ("dcte_kernels.hip", "1"),
     "DCTE_PF2_MAXN": ("dcte_kernels.hip", "2"),
     "DCTE_FIX_DIRECT8": ("dcte_kernels.hip", "128u"),
+    "DCTE_FIX_DIRECT4": ("dcte_kernels.hip", "64u"),
     "DCTE_FIX_IL": ("dcte_kernels.hip", "2"),
     "DCTE_FIX_GPS": ("dcte_kernels.hip", "1"),
     "DCTE_FIX_MINW": ("dcte_kernels.hip", "3"),
