@@ -118,6 +118,7 @@ struct dcte_ctx {
     unsigned dp_spin_limit = 0;     // DCTE_OPT_DP_SPIN_LIMIT (0: the kernel's default)
     unsigned long long* stamps = nullptr;   // DCTE_OPT_TSTAMP_BUF (timing-probe builds)
     int fail_inject = 0;            // DCTE_OPT_FAIL_INJECT (tests of the error paths)
+    bool exact = false;             // DCTE_OPT_EXACT
     std::vector<ProfEvent> prof;
     long long last_refined = 0;
     std::string last_error;
@@ -149,6 +150,11 @@ int bad_arg(dcte_ctx* ctx, const char* what)
     } while (0)
 
 bool valid_n(int n) { return n == 2 || n == 4 || n == 8 || n == 16; }
+
+// the refinement margin a call uses: the exact mode refines every pixel it
+// does not compute in fp64 outright (seam bands, points, and the block sizes /
+// semantics dcte_exact.hip has no sliding kernel for)
+double eff_tau(const dcte_ctx* ctx) { return ctx->exact ? 1.0 : ctx->tie_tau; }
 
 // window offsets -hl .. +hr of a semantics
 void halo(int n, int sem, int& hl, int& hr)
@@ -260,6 +266,63 @@ dcte::FixParams fix_params(const uint8_t* px, long long rowstride, int w, int h,
 
 int ensure_buf(dcte_ctx* ctx, void** p, size_t* cap, size_t bytes);
 
+// The exact map (DCTE_OPT_EXACT, dcte_exact.hip): one launch of the fp64
+// sliding-window kernel over the same row ranges, no refinement lists.  The
+// arguments were checked by run_device.
+int run_exact(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, int w, int h, int bpp,
+              int in_row0, int in_rows, int y0, int y1, int yb0, int yb1, int n, float edges,
+              float textures, int sem, float* d_out, long long out_stride, hipStream_t s)
+{
+    const int rows_a = y1 - y0, rows_b = yb1 - yb0;
+    int tile_h = ctx->tile_h > 0 ? ctx->tile_h : dcte::exact_default_tile_h(n);
+    if (tile_h > (rows_a > rows_b ? rows_a : rows_b)) tile_h = rows_a > rows_b ? rows_a : rows_b;
+    const int tiles_a = (rows_a + tile_h - 1) / tile_h;
+    const int tiles_y = tiles_a + (rows_b + tile_h - 1) / tile_h;
+    if (tiles_y > kMaxGridY) {
+        ctx->last_error = "tile rows exceed the launch grid (raise DCTE_OPT_TILE_H)";
+        return DCTE_ERANGE;
+    }
+    DCTE_HIP(ctx, hipSetDevice(d.id));
+    dcte::MapParams p{};
+    p.px = static_cast<const uint8_t*>(d_px);
+    p.rowstride = rowstride;
+    p.w = w;
+    p.h = h;
+    p.in_row0 = in_row0;
+    p.in_rows = in_rows;
+    p.y0 = y0;
+    p.y1 = y1;
+    p.yb0 = yb0;
+    p.yb1 = yb1;
+    p.tile_h = tile_h;
+    p.tiles_a = tiles_a;
+    p.tiles_y = tiles_y;
+    p.out = d_out;
+    p.out_stride = out_stride;
+    p.edges = edges;
+    p.textures = textures;
+    hipError_t e = hipSuccess;
+    if (ctx->profile) {
+        ProfEvent ev{d.id, nullptr, nullptr};
+        DCTE_HIP(ctx, hipEventCreate(&ev.a));
+        if ((e = hipEventCreate(&ev.b)) != hipSuccess) {
+            (void)hipEventDestroy(ev.a);
+            return hip_fail(ctx, e, "hipEventCreate");
+        }
+        ctx->prof.push_back(ev);      // dcte_profile_read destroys them
+        DCTE_HIP(ctx, hipEventRecord(ev.a, s));
+        DCTE_HIP(ctx, dcte::launch_map_exact(n, bpp, sem, p, s));
+        DCTE_HIP(ctx, hipEventRecord(ev.b, s));
+    } else {
+        DCTE_HIP(ctx, dcte::launch_map_exact(n, bpp, sem, p, s));
+    }
+    if (ctx->fail_inject == 1) {      // testing: the launch was queued, report it failed
+        ctx->fail_inject = 0;
+        return hip_fail(ctx, hipErrorLaunchFailure, "launch_map_exact (injected)");
+    }
+    return DCTE_OK;
+}
+
 // Output rows [y0, y1) -- plus [yb0, yb1) when yb0 < yb1 (y1 <= yb0: one
 // launch for both, the out row of y at d_out + (y - y0) * out_stride).
 int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, int w, int h,
@@ -290,6 +353,9 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     // shorter than a tile is one tile of exactly its rows (same results, and
     // the refinement list below is sized for the rows that exist)
     const int rows_a = y1 - y0, rows_b = yb1 - yb0;
+    const bool exact = ctx->exact && dcte::exact_supported(n, sem);
+    if (exact) return run_exact(ctx, d, d_px, rowstride, w, h, bpp, in_row0, in_rows, y0, y1, yb0, yb1, n,
+                                edges, textures, sem, d_out, out_stride, s);
     int tile_h = ctx->tile_h > 0 ? ctx->tile_h : dcte::map_default_tile_h(n);
     if (tile_h > (rows_a > rows_b ? rows_a : rows_b)) tile_h = rows_a > rows_b ? rows_a : rows_b;
     if ((long long)tile_h * out_stride * 4 >= (1LL << 31)) return DCTE_ERANGE;
@@ -353,7 +419,7 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     p.out_stride = out_stride;
     p.we = (float)((double)edges / scale);
     p.wt = (float)((double)textures / scale);
-    p.tie_tau = (float)ctx->tie_tau;
+    p.tie_tau = (float)eff_tau(ctx);
     p.edges = edges;
     p.textures = textures;
     p.fix_list = f->d_list;
@@ -404,7 +470,7 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     };
     if (injected(1)) return fail(hipErrorLaunchFailure, "launch_map (injected)");
     f->phase ^= 1u;   // the launch ran: the next one uses the counter it zeroed
-    if ((p.we != p.wt && ctx->tie_tau > 0) || ctx->tie_tau >= 1.0) {
+    if ((p.we != p.wt && eff_tau(ctx) > 0) || eff_tau(ctx) >= 1.0) {
         if ((e = dcte::launch_fix_tiles(n, bpp, sem, q, s)) != hipSuccess) return fail(e, "launch_fix_tiles");
         if (injected(2)) return fail(hipErrorLaunchFailure, "launch_fix_tiles (injected)");
     }
@@ -709,6 +775,13 @@ int dcte_set_option(dcte_ctx* ctx, int option, double value)
         if (!(value == 0 || value == 1 || value == 2)) return DCTE_EINVAL;
         ctx->fail_inject = (int)value;
         return DCTE_OK;
+    case DCTE_OPT_LEGACY_8:
+        // DCTE_OPT_WIDE_BANDS of the first release (removed; results never
+        // depended on it): still accepted, ignored
+        return DCTE_OK;
+    case DCTE_OPT_EXACT:
+        ctx->exact = value != 0;
+        return DCTE_OK;
     default: return DCTE_EINVAL;
     }
 }
@@ -781,13 +854,13 @@ int dcte_seam_carve_device(dcte_ctx* ctx, int device, const void* d_px, long lon
     p.map_out_stride = map_out_stride;
     p.we = (float)((double)edges / scale);
     p.wt = (float)((double)textures / scale);
-    p.tie_tau = (float)ctx->tie_tau;
+    p.tie_tau = (float)eff_tau(ctx);
     p.fix_count = f->d_count;
     p.fix_list = f->d_list;
     p.fix_cap = (unsigned)f->cap;
     DCTE_HIP(ctx, hipMemsetAsync(f->d_count, 0, sizeof(unsigned), s));
     DCTE_HIP(ctx, dcte::launch_seam_carve(p, s));
-    if ((p.we != p.wt && ctx->tie_tau > 0) || ctx->tie_tau >= 1.0) {
+    if ((p.we != p.wt && eff_tau(ctx) > 0) || eff_tau(ctx) >= 1.0) {
         dcte::FixParams q = fix_params(p.px_out, out_rowstride, w - 1, h, 0, bpp, n, 0, semantics,
                                        d_map_out, map_out_stride, edges, textures, f);
         DCTE_HIP(ctx, dcte::launch_fix(q, s));
@@ -828,13 +901,13 @@ int dcte_energy_points_device(dcte_ctx* ctx, int device, const void* d_px, long 
     p.map_out = d_out;
     p.we = (float)((double)edges / scale);
     p.wt = (float)((double)textures / scale);
-    p.tie_tau = (float)ctx->tie_tau;
+    p.tie_tau = (float)eff_tau(ctx);
     p.fix_count = f->d_count;
     p.fix_list = f->d_list;
     p.fix_cap = (unsigned)f->cap;
     DCTE_HIP(ctx, hipMemsetAsync(f->d_count, 0, sizeof(unsigned), s));
     DCTE_HIP(ctx, dcte::launch_points(p, s));
-    if ((p.we != p.wt && ctx->tie_tau > 0) || ctx->tie_tau >= 1.0) {
+    if ((p.we != p.wt && eff_tau(ctx) > 0) || eff_tau(ctx) >= 1.0) {
         dcte::FixParams q = fix_params(p.px, rowstride, w, h, 0, bpp, n, 0, semantics, d_out, 0,
                                        edges, textures, f);
         q.pts = d_xy;

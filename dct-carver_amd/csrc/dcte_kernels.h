@@ -189,4 +189,11 @@ int map_tiles_y(int n, int rows, int tile_h);
 int map_strips_per_tile(int n);
 int dense_batch_entries(int n, int sem);   // entries per dense refinement batch (0: no flat list)
 
+// the exact map (dcte_exact.hip, DCTE_OPT_EXACT): the reference's fp64
+// arithmetic in a sliding window, no refinement launch
+hipError_t launch_map_exact(int n, int bpp, int sem, const MapParams& p, hipStream_t s);
+bool exact_supported(int n, int sem);   // else the exact mode refines every pixel of the fp32 map
+int exact_tile_w(int n);                // output columns per workgroup
+int exact_default_tile_h(int n);
+
 }  // namespace dcte

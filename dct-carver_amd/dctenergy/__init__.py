@@ -36,7 +36,9 @@ DCTE_OPT_TILE_H = 4
 DCTE_OPT_DP_BANDWISE = 5
 DCTE_OPT_DP_SPIN_LIMIT = 6
 DCTE_OPT_TSTAMP_BUF = 7
-DCTE_OPT_FAIL_INJECT = 8
+DCTE_OPT_LEGACY_8 = 8
+DCTE_OPT_FAIL_INJECT = 9
+DCTE_OPT_EXACT = 10
 DCTE_NORM_LQR = 0
 DCTE_NORM_PREVIEW = 1
 DCTE_CREATE_SAME_DEVICE = 1
@@ -211,9 +213,10 @@ class Context:
     """One dcte_ctx (a set of devices).  Not thread-safe, like the reference
     callback (src/render.c:140 shares params->data)."""
 
-    def __init__(self, ngpus=0, tie_tau=None, same_device=False):
+    def __init__(self, ngpus=0, tie_tau=None, same_device=False, exact=False):
         """same_device: `ngpus` logical devices that are all device 0
-        (DCTE_CREATE_SAME_DEVICE) -- the multi-device host path on one GPU."""
+        (DCTE_CREATE_SAME_DEVICE) -- the multi-device host path on one GPU.
+        exact: DCTE_OPT_EXACT (every pixel bit-identical to the reference)."""
         L = lib()
         h = ctypes.c_void_p()
         rc = L.dcte_create(ctypes.byref(h), ngpus,
@@ -223,6 +226,8 @@ class Context:
         self._h = h
         if tie_tau is not None:
             self.set_option(DCTE_OPT_TIE_TAU, tie_tau)
+        if exact:
+            self.set_option(DCTE_OPT_EXACT, 1)
 
     # -- lifecycle
     def close(self):
@@ -546,5 +551,5 @@ class Carver:
 
 __all__ = ["Context", "Carver", "DcteError", "lib", "device_count", "LIB_PATH", "EXPORTS",
            "energy_window", "normalize_u8_host",
-           "DCTE_LQR", "DCTE_PREVIEW", "DCTE_OPT_TIE_TAU", "DCTE_OPT_PROFILE", "DCTE_OPT_PIN_HOST", "DCTE_OPT_TILE_H", "DCTE_OPT_DP_BANDWISE", "DCTE_OPT_DP_SPIN_LIMIT",
+           "DCTE_LQR", "DCTE_PREVIEW", "DCTE_OPT_TIE_TAU", "DCTE_OPT_EXACT", "DCTE_OPT_FAIL_INJECT", "DCTE_OPT_PROFILE", "DCTE_OPT_PIN_HOST", "DCTE_OPT_TILE_H", "DCTE_OPT_DP_BANDWISE", "DCTE_OPT_DP_SPIN_LIMIT",
            "DCTE_NORM_LQR", "DCTE_NORM_PREVIEW"]

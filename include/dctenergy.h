@@ -96,10 +96,24 @@ extern "C" {
                                only: device address of a buffer of 3 uint64
                                per map workgroup {start, end, HW_ID}; 0 = none.
                                Product builds ignore it. */
-#define DCTE_OPT_FAIL_INJECT 8 /* testing the error paths: 1 = the next map
+#define DCTE_OPT_LEGACY_8 8  /* DCTE_OPT_WIDE_BANDS of the first release
+                               (removed): accepted and ignored, as its results
+                               never depended on it */
+#define DCTE_OPT_FAIL_INJECT 9 /* testing the error paths: 1 = the next map
                                launch is reported as failed (DCTE_EHIP) right
                                after it was queued; 2 = the next refinement
                                launch likewise.  One-shot; 0 = off. */
+#define DCTE_OPT_EXACT 10   /* 1 = bit-identical to the reference for every
+                               pixel: the map is computed in the reference's
+                               own fp64 operation order (ddct8x8s / ddct16x16s /
+                               ddct2d and the last-maximum scan) by a sliding-
+                               window kernel, so liblqr's DP on it carves the
+                               reference's seams.  Where no such kernel exists
+                                every pixel of the fp32 map is
+                               refined in fp64 instead -- the same bits, slower.
+                               Seam-band updates and point energies are then
+                               refined in fp64 too.  0 = the fp32 map with the
+                               tie refinement (default; <= 1e-5 relative). */
 
 typedef struct dcte_ctx dcte_ctx;
 

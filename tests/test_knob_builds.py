@@ -40,6 +40,8 @@ KNOBS = {
     "DCTE_DENSE_OVERSUB": ("dcte_kernels.hip", "1"),
     "DCTE_DENSE_OVERSUB_MEMO": ("dcte_kernels.hip", "16"),
     "DCTE_MEMO_SLOTS": ("dcte_kernels.hip", "64"),
+    "DCTE_EX_TILE_H": ("dcte_exact.hip", "64"),
+    "DCTE_EX_MINW": ("dcte_exact.hip", "1"),
     "DCTE_SHIFT_VEC": ("dcte_seam.hip", "1"),
     "DCTE_DP_C": ("dcte_dp.hip", "1"),
     "DCTE_DP_R": ("dcte_dp.hip", "16"),

@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "dct-carver_amd")]
 
 
-def load(path):
+def load(path, exact=False):
     L = ctypes.CDLL(path)
     vp = ctypes.c_void_p
     L.dcte_create.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_uint]
@@ -29,6 +29,8 @@ def load(path):
     h = vp()
     assert L.dcte_create(ctypes.byref(h), 1, 0) == 0
     L.dcte_set_option(h, 2, 1.0)
+    if exact:
+        assert L.dcte_set_option(h, 10, 1.0) == 0          # DCTE_OPT_EXACT
     return L, h
 
 
@@ -46,6 +48,7 @@ def main():
     ap.add_argument("--check", type=int, default=0,
                     help="also map a CHECKxCHECK natural frame and a dots-on-flat frame with "
                          "every build and compare with the CPU oracle (tolerance, class flips)")
+    ap.add_argument("--exact", action="store_true", help="DCTE_OPT_EXACT (the fp64 map)")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     import torch
@@ -54,7 +57,7 @@ def main():
     frame = synth.natural_rows(0, S, S, a.bpp, seed=0, device="cuda")
     out = torch.empty((S, S), dtype=torch.float32, device="cuda")
     ref = None
-    libs = [(p, *load(p)) for p in a.libs]
+    libs = [(p, *load(p, a.exact)) for p in a.libs]
     stream = torch.cuda.current_stream().cuda_stream
     times = {p: [] for p in a.libs}
     same = {}
@@ -118,7 +121,7 @@ def main():
             checks[p] = {"check_off_tol": bad, "check_flips": flips, "check_max_rel": worst}
     for p in a.libs:
         t = times[p]
-        print(json.dumps({"lib": os.path.basename(p), "n": a.n, "size": S, "e2e": a.e2e,
+        print(json.dumps({"lib": os.path.basename(p), "n": a.n, "size": S, "e2e": a.e2e, "exact": a.exact,
                           "median_ms": round(statistics.median(t), 4), "min_ms": round(min(t), 4),
                           "mpx_s": round(S * S / statistics.median(t) / 1e3, 1),
                           "bit_equal_first": same[p], **checks.get(p, {})}))

@@ -9,7 +9,7 @@ BASE="-O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -fPIC --offload-arch=g
 build() {  # name extra-flags...
   local name=$1; shift
   local objs=""
-  for src in csrc/dcte_kernels.hip csrc/dcte_norm.hip csrc/dcte_seam.hip csrc/dcte_dp.hip csrc/dcte_capi.cpp; do
+  for src in csrc/dcte_kernels.hip csrc/dcte_exact.hip csrc/dcte_norm.hip csrc/dcte_seam.hip csrc/dcte_dp.hip csrc/dcte_capi.cpp; do
     local o=build/variants/$name.$(basename $src).o
     $HIPCC $BASE "$@" -c -o $o $src
     objs="$objs $o"
