@@ -301,6 +301,7 @@ int run_exact(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, i
     p.out_stride = out_stride;
     p.edges = edges;
     p.textures = textures;
+    small_twiddles(n, p.ct);
     hipError_t e = hipSuccess;
     if (ctx->profile) {
         ProfEvent ev{d.id, nullptr, nullptr};

@@ -44,7 +44,10 @@ namespace {
 #define DCTE_EX_TILE_H 128   // output rows per workgroup
 #endif
 #ifndef DCTE_EX_MINW
-#define DCTE_EX_MINW 2       // waves per SIMD the register budget is cut for (<= 256 VGPRs)
+#define DCTE_EX_MINW 2       // N = 8: waves per SIMD the register budget is cut for (<= 256 VGPRs)
+#endif
+#ifndef DCTE_EX16_MINW
+#define DCTE_EX16_MINW 4     // N = 16 (8-wave workgroups: 4 = two of them per CU, <= 128 VGPRs)
 #endif
 
 constexpr unsigned kRawFlags = 0x00020000u;   // gfx9 raw buffer dword3
@@ -61,6 +64,17 @@ __device__ __forceinline__ void sfor(F&& f)
 }
 
 __device__ __forceinline__ int clampx(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// the weight of a decision: edges or textures, selected in registers.  The
+// operands go through an empty asm so the optimiser cannot turn the select
+// into a load through a selected address (it did: the weights live in the
+// lambdas' closures, and a select between two loads from them became a
+// dynamically indexed closure, i.e. scratch memory)
+__device__ __forceinline__ double weight(bool edge, double we, double wt)
+{
+    asm volatile("" : "+v"(we), "+v"(wt));
+    return edge ? we : wt;
+}
 
 using r64::K8;
 
@@ -115,11 +129,15 @@ __device__ __forceinline__ void col8(double v0, double v1, double v2, double v3,
 struct Frame {
     __amdgpu_buffer_rsrc_t rsrc;
     uint32_t base_off, nrec4, tail;
+    long long rowstride;
+    int in_row0;
     bool tail_wg;
 
     __device__ __forceinline__ void init(const MapParams& p, int bpp, bool reaches_end)
     {
         const uintptr_t pbase = reinterpret_cast<uintptr_t>(p.px);
+        rowstride = p.rowstride;
+        in_row0 = p.in_row0;
         base_off = (uint32_t)(pbase & 3u);
         const unsigned nrec = base_off + (unsigned)((long long)(p.in_rows - 1) * p.rowstride) +
                               (unsigned)(p.w * bpp);
@@ -134,9 +152,9 @@ struct Frame {
         }
     }
     // byte offset (from the aligned base) of pixel (x, global row y)
-    __device__ __forceinline__ uint32_t at(const MapParams& p, int x, int y, int bpp) const
+    __device__ __forceinline__ uint32_t at(int x, int y, int bpp) const
     {
-        return base_off + (uint32_t)((long long)(y - p.in_row0) * p.rowstride) + (uint32_t)(x * bpp);
+        return base_off + (uint32_t)((long long)(y - in_row0) * rowstride) + (uint32_t)(x * bpp);
     }
     // the 8 bytes from the dword holding byte a on
     __device__ __forceinline__ uint2 fetch(uint32_t a) const
@@ -175,6 +193,18 @@ __device__ __forceinline__ double luma_of(const double* lut, uint32_t wd)
     else return (lut[wd & 255u] + lut[256 + ((wd >> 8) & 255u)]) + lut[512 + ((wd >> 16) & 255u)];
 }
 
+// first / one-past-last output row of tile row by (tile_row0 / tile_row1 of
+// dcte_kernels.h) in arithmetic: a select between two fields of the kernel
+// argument is folded into a load through a selected address, which keeps the
+// whole argument block in scratch memory
+__device__ __forceinline__ void tile_rows(const MapParams& p, int by, int& ys, int& ye)
+{
+    const int second = by >= p.tiles_a;                // 0 / 1
+    const int r0 = p.y0 + second * (p.yb0 - p.y0), e = p.y1 + second * (p.yb1 - p.y1);
+    ys = r0 + (by - second * p.tiles_a) * p.tile_h;
+    ye = min(ys + p.tile_h, e);
+}
+
 // XCD-aware tile order (as dcte_map): each XCD gets a contiguous run of tiles
 __device__ __forceinline__ void xcd_tile(int& bx, int& by)
 {
@@ -209,7 +239,8 @@ __global__ __launch_bounds__(kEx8T, DCTE_EX_MINW) void dcte_exact8(const MapPara
     int bx, by;
     xcd_tile(bx, by);
     const int x0 = bx * T, x = x0 + tx;
-    const int ys = tile_row0(p, by), ye = tile_row1(p, by);
+    int ys, ye;
+    tile_rows(p, by, ys, ye);
     const int n_in = (ye - ys) + N - 1;
     const int ngroups = (n_in + G - 1) / G;
     const int w = p.w, h = p.h;
@@ -229,17 +260,17 @@ __global__ __launch_bounds__(kEx8T, DCTE_EX_MINW) void dcte_exact8(const MapPara
     uint2 pend[G], hpend = make_uint2(0u, 0u);
     auto issue = [&](int g) __attribute__((always_inline)) {
 #pragma unroll
-        for (int u = 0; u < G; u++) pend[u] = fr.fetch(fr.at(p, xc, row_of(g * G + u), BPP));
-        if (has_halo) hpend = fr.fetch(fr.at(p, hxc, row_of(g * G + hrow), BPP));
+        for (int u = 0; u < G; u++) pend[u] = fr.fetch(fr.at(xc, row_of(g * G + u), BPP));
+        if (has_halo) hpend = fr.fetch(fr.at(hxc, row_of(g * G + hrow), BPP));
     };
     auto convert = [&](int g, int b) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < G; u++) {
-            const uint32_t off = fr.at(p, xc, row_of(g * G + u), BPP) & 3u;
+            const uint32_t off = fr.at(xc, row_of(g * G + u), BPP) & 3u;
             lum[b][u][tx] = luma_of<BPP>(lut, __builtin_amdgcn_alignbyte(pend[u].y, pend[u].x, off));
         }
         if (has_halo) {
-            const uint32_t off = fr.at(p, hxc, row_of(g * G + hrow), BPP) & 3u;
+            const uint32_t off = fr.at(hxc, row_of(g * G + hrow), BPP) & 3u;
             lum[b][hrow][T + hl % XH] = luma_of<BPP>(lut, __builtin_amdgcn_alignbyte(hpend.y, hpend.x, off));
         }
     };
@@ -250,7 +281,7 @@ __global__ __launch_bounds__(kEx8T, DCTE_EX_MINW) void dcte_exact8(const MapPara
     double ring[N][N];                                // ring[slot][k1], slot = input row mod 8
 
     auto compute = [&](int g, int b) __attribute__((always_inline)) {
-        sfor<G>([&](auto U) {
+        sfor<G>([&](auto U) __attribute__((always_inline)) {
             constexpr int u = decltype(U)::value;
             const int i = g * G + u;
             if (i < n_in) {
@@ -281,7 +312,7 @@ __global__ __launch_bounds__(kEx8T, DCTE_EX_MINW) void dcte_exact8(const MapPara
                     // nothing in (0,2..7) holds it and |C01| = M)
                     const double M = fmax(fmax(mp, a10), fmax(m0, a01));
                     const bool edge = !(mp == M) && (a10 == M || (!(m0 == M) && a01 == M));
-                    const float e = (float)(M * (edge ? we : wt));
+                    const float e = (float)(M * weight(edge, we, wt));
                     if (inside) orow[(long long)(i - (N - 1)) * p.out_stride] = e;
                 }
             }
@@ -307,10 +338,447 @@ hipError_t launch_exact8(const MapParams& p, hipStream_t s)
     return hipGetLastError();
 }
 
+
+// ------------------------------------------------------------------ N = 16
+// ddct16x16s (shrtdct.c:231-386): the same sliding structure with a 16-row
+// ring of 16 channels per column -- 256 doubles, so a column is split over
+// EIGHT waves, wave q holding the two channels (k1) one rotation of the
+// reference's pass-1 step produces together:
+//   q = 0: k1 = 0, 8    q = 1: 4, 12    q = 2: 2, 14    q = 3: 6, 10
+//   q = 4: 1, 15        q = 5: 7, 9     q = 6: 5, 11    q = 7: 3, 13
+// (a 2 x 16 register ring, 64 VGPRs).  Each wave runs only the part of the
+// pass-1 step its pair needs (sums for q < 4, differences for q >= 4, then its
+// rotation; 18-40 of the step's 114 operations), and the pass-2 steps of its
+// two channels.  The eight partial maxima of a pixel meet in LDS: the post-
+// (1,0) maximum by a 64-bit LDS atomic max on the (non-negative) doubles'
+// bits, |C01|, max |C0,2..15| and |C10| in slots of their own; after the
+// group's barrier wave q decides rows u = q, q + 8 of the group.
+constexpr int kEx16W = 8;                          // waves per workgroup
+constexpr int kEx16T = 64 * kEx16W;
+constexpr int kEx16LW = 64 + 15;                   // luma columns of a 64-column strip
+constexpr int kEx16G = 16;                         // rows per group (= ring depth)
+constexpr int kEx16Conv = (kEx16G * kEx16LW + kEx16T - 1) / kEx16T;   // conversions per lane and group
+
+using r64::K16;
+
+// pass 1 of ddct16x16s (shrtdct.c:239-313) on window line v, only the two
+// outputs of wave q (k1 = kA, kB above); q is wave-uniform
+__device__ __forceinline__ void row16_pair(int q, const double (&v)[16], double& oa, double& ob)
+{
+    double xr, xi;
+    if (q < 4) {
+        const double s0 = v[0] + v[15], t0 = v[8] + v[7];
+        const double s1 = v[2] + v[13], t1 = v[10] + v[5];
+        const double s2 = v[4] + v[11], t2 = v[12] + v[3];
+        const double s3 = v[6] + v[9], t3 = v[14] + v[1];
+        if (q < 2) {
+            const double x0r = s0 + t0, x1r = s1 + t1, x2r = s2 + t2, x3r = s3 + t3;
+            if (q == 0) {                                  // k1 = 0, 8
+                xr = x0r + x2r;
+                xi = x1r + x3r;
+                oa = K16::c8 * (xr + xi);
+                ob = K16::c8 * (xr - xi);
+            } else {                                       // k1 = 4, 12
+                xr = x0r - x2r;
+                xi = x1r - x3r;
+                oa = K16::c4 * xr - K16::s4 * xi;
+                ob = K16::c4 * xi + K16::s4 * xr;
+            }
+        } else {
+            const double x0i = s0 - t0, x1i = s1 - t1, x2i = s2 - t2, x3i = s3 - t3;
+            const double y0r = K16::w8 * (x1i - x3i), y2r = K16::w8 * (x1i + x3i);
+            if (q == 2) {                                  // k1 = 2, 14
+                xr = x0i + y0r;
+                xi = y2r + x2i;
+                oa = K16::c2 * xr - K16::s2 * xi;
+                ob = K16::c2 * xi + K16::s2 * xr;
+            } else {                                       // k1 = 6, 10
+                xr = x0i - y0r;
+                xi = y2r - x2i;
+                oa = K16::c6 * xr - K16::s6 * xi;
+                ob = K16::c6 * xi + K16::s6 * xr;
+            }
+        }
+    } else {
+        const double x4r = v[0] - v[15], x4i = v[8] - v[7];
+        const double x5r = v[2] - v[13], x5i = v[10] - v[5];
+        const double x6r = v[4] - v[11], x6i = v[12] - v[3];
+        const double x7r = v[6] - v[9], x7i = v[14] - v[1];
+        xr = K16::w8 * (x6r - x6i);
+        xi = K16::w8 * (x6i + x6r);
+        const double y6r = x4r - xr, y6i = x4i - xi, y4r = x4r + xr, y4i = x4i + xi;
+        xr = K16::w4s * x7r - K16::w4c * x7i;
+        xi = K16::w4s * x7i + K16::w4c * x7r;
+        const double y7r = K16::w4c * x5r - K16::w4s * x5i;
+        const double y7i = K16::w4c * x5i + K16::w4s * x5r;
+        const double y5r = y7r + xr, y5i = y7i + xi, z7r = y7r - xr, z7i = y7i - xi;
+        double c, sn;
+        if (q == 4) {                                      // k1 = 1, 15
+            xr = y4r + y5r;
+            xi = y5i + y4i;
+            c = K16::c1;
+            sn = K16::s1;
+        } else if (q == 5) {                               // k1 = 7, 9
+            xr = y4r - y5r;
+            xi = y5i - y4i;
+            c = K16::c7;
+            sn = K16::s7;
+        } else if (q == 6) {                               // k1 = 5, 11
+            xr = y6r - z7i;
+            xi = z7r + y6i;
+            c = K16::c5;
+            sn = K16::s5;
+        } else {                                           // k1 = 3, 13
+            xr = y6r + z7i;
+            xi = z7r - y6i;
+            c = K16::c3;
+            sn = K16::s3;
+        }
+        oa = c * xr - sn * xi;
+        ob = c * xi + sn * xr;
+    }
+}
+
+// pass 2 of ddct16x16s (shrtdct.c:314-386) on coefficient row k1 (v[j] =
+// a[k1][j]): acc = max over |C_k1,k2| for k2 in {2..7, 9..15}; x0 / x1 = the
+// pair C_k1,0 = c8 (x0 + x1), C_k1,8 = c8 (x0 - x1) is formed from; c1 = C_k1,1
+__device__ __forceinline__ void col16(const double (&v)[16], double& acc, double& x0, double& x1, double& c1)
+{
+    const double x4r = v[0] - v[15], sr0 = v[0] + v[15];
+    const double x4i = v[8] - v[7], si0 = v[8] + v[7];
+    const double x0r = sr0 + si0, x0i = sr0 - si0;
+    const double x5r = v[2] - v[13], sr1 = v[2] + v[13];
+    const double x5i = v[10] - v[5], si1 = v[10] + v[5];
+    const double x1r = sr1 + si1, x1i = sr1 - si1;
+    const double x6r = v[4] - v[11], sr2 = v[4] + v[11];
+    const double x6i = v[12] - v[3], si2 = v[12] + v[3];
+    const double x2r = sr2 + si2, x2i = sr2 - si2;
+    const double x7r = v[6] - v[9], sr3 = v[6] + v[9];
+    const double x7i = v[14] - v[1], si3 = v[14] + v[1];
+    const double x3r = sr3 + si3, x3i = sr3 - si3;
+    x0 = x0r + x2r;
+    x1 = x1r + x3r;
+    double xr = x0r - x2r, xi = x1r - x3r;
+    double a = fmax(fabs(K16::c4 * xr - K16::s4 * xi), fabs(K16::c4 * xi + K16::s4 * xr));   // C4, C12
+    const double y0r = K16::w8 * (x1i - x3i), y2r = K16::w8 * (x1i + x3i);
+    xr = x0i + y0r;
+    xi = y2r + x2i;
+    a = fmax(a, fabs(K16::c2 * xr - K16::s2 * xi));        // C2
+    a = fmax(a, fabs(K16::c2 * xi + K16::s2 * xr));        // C14
+    xr = x0i - y0r;
+    xi = y2r - x2i;
+    a = fmax(a, fabs(K16::c6 * xr - K16::s6 * xi));        // C6
+    a = fmax(a, fabs(K16::c6 * xi + K16::s6 * xr));        // C10
+    xr = K16::w8 * (x6r - x6i);
+    xi = K16::w8 * (x6i + x6r);
+    const double y6r = x4r - xr, y6i = x4i - xi, y4r = x4r + xr, y4i = x4i + xi;
+    xr = K16::w4s * x7r - K16::w4c * x7i;
+    xi = K16::w4s * x7i + K16::w4c * x7r;
+    const double y7r = K16::w4c * x5r - K16::w4s * x5i;
+    const double y7i = K16::w4c * x5i + K16::w4s * x5r;
+    const double y5r = y7r + xr, y5i = y7i + xi, z7r = y7r - xr, z7i = y7i - xi;
+    xr = y4r + y5r;
+    xi = y5i + y4i;
+    c1 = K16::c1 * xr - K16::s1 * xi;                      // C1
+    a = fmax(a, fabs(K16::c1 * xi + K16::s1 * xr));        // C15
+    xr = y4r - y5r;
+    xi = y5i - y4i;
+    a = fmax(a, fabs(K16::c7 * xr - K16::s7 * xi));        // C7
+    a = fmax(a, fabs(K16::c7 * xi + K16::s7 * xr));        // C9
+    xr = y6r - z7i;
+    xi = z7r + y6i;
+    a = fmax(a, fabs(K16::c5 * xr - K16::s5 * xi));        // C5
+    a = fmax(a, fabs(K16::c5 * xi + K16::s5 * xr));        // C11
+    xr = y6r + z7i;
+    xi = z7r - y6i;
+    a = fmax(a, fabs(K16::c3 * xr - K16::s3 * xi));        // C3
+    a = fmax(a, fabs(K16::c3 * xi + K16::s3 * xr));        // C13
+    acc = a;
+}
+
+template <int BPP>
+__global__ __launch_bounds__(kEx16T, DCTE_EX16_MINW) void dcte_exact16(const MapParams p)
+{
+    constexpr int N = 16, HL = 7, HR = 8, G = kEx16G, LW = kEx16LW, T = kEx16T;
+    __shared__ double lut[BPP == 1 ? 256 : 768];
+    __shared__ double lum[G][LW];
+    __shared__ unsigned long long pmax[G][64];      // max |C| after (1,0), as bits (atomic max)
+    __shared__ double pe[G][3][64];                 // |C01|, max |C0,2..15|, |C10|
+
+    const int tx = threadIdx.x, c = tx & 63;
+    const int q = __builtin_amdgcn_readfirstlane(tx >> 6);   // wave = channel pair
+    int bx, by;
+    xcd_tile(bx, by);
+    const int x0 = bx * 64, x = x0 + c;
+    int ys, ye;
+    tile_rows(p, by, ys, ye);
+    const int n_in = (ye - ys) + N - 1;
+    const int ngroups = (n_in + G - 1) / G;
+    const int w = p.w, h = p.h;
+
+    Frame fr;
+    fr.init(p, BPP, x0 + 64 + HR - 1 >= w - 1 && min(h - 1, ye - 1 + HR) >= p.in_row0 + p.in_rows - 1);
+    fill_lut<BPP>(lut, tx, T);
+    for (int e = tx; e < G * 64; e += T) pmax[e / 64][e % 64] = 0ull;
+
+    auto row_of = [&](int i) { return clampx(ys - HL + (i < n_in ? i : n_in - 1), 0, h - 1); };
+    // the lane's luma conversions of a group: (row, column) pairs e = tx + T k
+    int crow[kEx16Conv], ccol[kEx16Conv], cxc[kEx16Conv];
+#pragma unroll
+    for (int k = 0; k < kEx16Conv; k++) {
+        const int e = tx + T * k;
+        crow[k] = e < G * LW ? e / LW : -1;
+        ccol[k] = e < G * LW ? e % LW : 0;
+        cxc[k] = clampx(x0 - HL + ccol[k], 0, w - 1);
+    }
+    uint2 pend[kEx16Conv];
+    auto issue = [&](int g) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < kEx16Conv; k++)
+            if (crow[k] >= 0) pend[k] = fr.fetch(fr.at(cxc[k], row_of(g * G + crow[k]), BPP));
+    };
+    auto convert = [&](int g) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < kEx16Conv; k++) {
+            if (crow[k] >= 0) {
+                const uint32_t off = fr.at(cxc[k], row_of(g * G + crow[k]), BPP) & 3u;
+                lum[crow[k]][ccol[k]] = luma_of<BPP>(lut, __builtin_amdgcn_alignbyte(pend[k].y, pend[k].x, off));
+            }
+        }
+    };
+
+    const double we = (double)p.edges, wt = (double)p.textures;
+    double ring[N][2];
+
+    auto compute = [&](int g) __attribute__((always_inline)) {
+        sfor<G>([&](auto U) __attribute__((always_inline)) {
+            constexpr int u = decltype(U)::value;
+            const int i = g * G + u;
+            if (i < n_in) {
+                double v[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) v[k] = lum[u][c + k];
+                row16_pair(q, v, ring[u][0], ring[u][1]);
+                if (i >= N - 1) {
+                    // window line j = input row i - 15 + j = slot (u + 1 + j) % 16
+                    double va[16], vb[16];
+#pragma unroll
+                    for (int j = 0; j < 16; j++) {
+                        va[j] = ring[(u + 1 + j) % 16][0];
+                        vb[j] = ring[(u + 1 + j) % 16][1];
+                    }
+                    double accb, b0, b1, bc1;
+                    col16(vb, accb, b0, b1, bc1);      // channel B: never an edge atom's row
+                    double mp = fmax(fmax(accb, fabs(bc1)), K16::c8 * (fabs(b0) + fabs(b1)));
+                    double acca, a0, a1, ac1;
+                    col16(va, acca, a0, a1, ac1);
+                    if (q == 0) {                      // k1 = 0: C01 and C0,2..15 (C00 not scanned)
+                        pe[u][0][c] = fabs(ac1);
+                        pe[u][1][c] = fmax(acca, fabs(K16::c8 * (a0 - a1)));
+                    } else if (q == 4) {               // k1 = 1: C10 apart
+                        pe[u][2][c] = fabs(K16::c8 * (a0 + a1));
+                        mp = fmax(mp, fmax(fmax(acca, fabs(ac1)), fabs(K16::c8 * (a0 - a1))));
+                    } else {
+                        mp = fmax(mp, fmax(fmax(acca, fabs(ac1)), K16::c8 * (fabs(a0) + fabs(a1))));
+                    }
+                    atomicMax(&pmax[u][c], (unsigned long long)__double_as_longlong(mp));
+                }
+            }
+        });
+    };
+    auto finalize = [&](int g) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            const int u = q + 8 * r, i = g * G + u;
+            if (i >= N - 1 && i < n_in) {
+                const double mp = __longlong_as_double((long long)pmax[u][c]);
+                const double a01 = pe[u][0][c], m0 = pe[u][1][c], a10 = pe[u][2][c];
+                const double M = fmax(fmax(mp, a10), fmax(m0, a01));
+                const bool edge = !(mp == M) && (a10 == M || (!(m0 == M) && a01 == M));
+                if (x < w) p.out[(long long)(ys + i - (N - 1) - p.y0) * p.out_stride + x] = (float)(M * weight(edge, we, wt));
+            }
+            pmax[u][c] = 0ull;
+        }
+    };
+
+    issue(0);
+    for (int g = 0; g < ngroups; g++) {
+        convert(g);
+        if (g + 1 < ngroups) issue(g + 1);
+        __syncthreads();             // lum of g; the previous group's decisions done
+        compute(g);
+        __syncthreads();             // partials of g; every read of lum done
+        finalize(g);
+    }
+}
+
+template <int BPP>
+hipError_t launch_exact16(const MapParams& p, hipStream_t s)
+{
+    dim3 grid((p.w + 63) / 64, p.tiles_y);
+    hipLaunchKernelGGL((dcte_exact16<BPP>), grid, dim3(kEx16T), 0, s, p);
+    return hipGetLastError();
+}
+
+
+// ------------------------------------------------------------------ N = 2, 4
+// dctNxN calls ddct2d here (src/dct.c:82-85, src/fft2d/fftsg2d.c:566-627):
+// ddct (fftsg.c:349-402) along the SECOND index first -- dy, a vertical
+// transform of each window column -- then along the first.  The vertical
+// transform V(x', y) of image column x' over the window rows is the same
+// doubles for the N pixels x' - HR .. x' + HL whose windows hold that column,
+// so it is computed once per (column, row) and shared ACROSS lanes: a wave owns
+// 64 consecutive columns, lane l computes V of its column from a register ring
+// of the column's last N luma values, the wave swaps the V vectors through a
+// wave-private LDS row, and lanes 0 .. 64 - N each run the N horizontal
+// transforms of their pixel (the last N - 1 lanes only supply V).  No
+// workgroup barrier after the luma tables.
+constexpr int kExST = 256;                         // 4 independent waves
+
+// ddct(n, -1) on v[0..n-1] (dcte_ref64.h step_small: fftsg.c ddct with
+// cftx020 / dctsub for n = 4, the makect twiddles ct)
+template <int N>
+__device__ __forceinline__ void ddct_small(double (&v)[N], const double* ct, double wkr, double wki)
+{
+    if constexpr (N == 2) {
+        const double t = v[1];
+        v[1] = v[0] - t;
+        v[0] += t;
+        v[1] *= ct[0];
+    } else {
+        double a0 = v[0], a1 = v[1], a2 = v[2], a3 = v[3];
+        const double t = a3;
+        a3 = a2 - a1;
+        a2 += a1;
+        a1 = a0 - t;
+        a0 += t;
+        const double x0r = a0 - a2, x0i = a1 - a3;    // cftx020
+        a0 += a2;
+        a1 += a3;
+        a2 = x0r;
+        a3 = x0i;
+        const double xr = wki * a1 - wkr * a3;        // dctsub
+        a1 = wkr * a1 + wki * a3;
+        a3 = xr;
+        a2 *= ct[0];
+        v[0] = a0;
+        v[1] = a1;
+        v[2] = a2;
+        v[3] = a3;
+    }
+}
+
+template <int N, int BPP>
+__global__ __launch_bounds__(kExST) void dcte_exact_small(const MapParams p)
+{
+    constexpr int HL = N / 2 - 1, HR = N / 2, G = 8, OW = 64 - (N - 1);
+    __shared__ double lut[BPP == 1 ? 256 : 768];
+    __shared__ double vrow[kExST / 64][2][N][64];   // per wave, by row parity: V[k2][lane]
+
+    const int tx = threadIdx.x, l = tx & 63, wv = tx >> 6;
+    int bx, by;
+    xcd_tile(bx, by);
+    const int xs = (bx * (kExST / 64) + wv) * OW;      // first output column of the wave
+    const int x = xs + l;
+    int ys, ye;
+    tile_rows(p, by, ys, ye);
+    const int n_in = (ye - ys) + N - 1;
+    const int ngroups = (n_in + G - 1) / G;
+    const int w = p.w, h = p.h;
+    const int xcol = clampx(x - HL, 0, w - 1);         // lane l's column: x - HL
+
+    Frame fr;
+    fr.init(p, BPP, (bx + 1) * (kExST / 64) * OW + 64 >= w && min(h - 1, ye - 1 + HR) >= p.in_row0 + p.in_rows - 1);
+    fill_lut<BPP>(lut, tx, kExST);
+    const double ct[2] = {p.ct[0], 0.0};
+    const double wkr = p.ct[1] - p.ct[3], wki = p.ct[1] + p.ct[3];   // dctsub's k = 1 twiddle
+    const double we = (double)p.edges, wt = (double)p.textures;
+    __syncthreads();
+    if (xs >= w) return;                               // wave-uniform; no barrier follows
+
+    auto row_of = [&](int i) { return clampx(ys - HL + (i < n_in ? i : n_in - 1), 0, h - 1); };
+    uint2 pend[2][G];
+    auto issue = [&](int g, int b) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < G; u++) pend[b][u] = fr.fetch(fr.at(xcol, row_of(g * G + u), BPP));
+    };
+    double ring[N];                                    // luma of the column's last N input rows
+    const bool emits = l < OW && x < w;
+    float* const orow = p.out + (long long)(ys - p.y0) * p.out_stride + x;
+
+    auto compute = [&](int g, int b) __attribute__((always_inline)) {
+        sfor<G>([&](auto U) __attribute__((always_inline)) {
+            constexpr int u = decltype(U)::value;
+            const int i = g * G + u;
+            if (i < n_in) {
+                const uint32_t off = fr.at(xcol, row_of(i), BPP) & 3u;
+                ring[u % N] = luma_of<BPP>(lut, __builtin_amdgcn_alignbyte(pend[b][u].y, pend[b][u].x, off));
+                if (i >= N - 1) {
+                    // pass 1 along dy: window line j = input row i - N + 1 + j
+                    double v[N];
+#pragma unroll
+                    for (int j = 0; j < N; j++) v[j] = ring[(u + 1 + j) % N];
+                    ddct_small<N>(v, ct, wkr, wki);
+                    double* vr = &vrow[wv][u & 1][0][0];
+#pragma unroll
+                    for (int k = 0; k < N; k++) vr[k * 64 + l] = v[k];
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    // pass 2 along dx for each k2, over lanes l .. l + N - 1
+                    const int ll = l < OW ? l : OW - 1;
+                    double a01 = 0.0, m0 = -1.0, a10 = 0.0, mp = 0.0;
+#pragma unroll
+                    for (int k2 = 0; k2 < N; k2++) {
+                        double hv[N];
+#pragma unroll
+                        for (int j = 0; j < N; j++) hv[j] = vr[k2 * 64 + ll + j];
+                        ddct_small<N>(hv, ct, wkr, wki);
+                        // C[k1][k2] = hv[k1]; scan order k1 outer, k2 inner
+#pragma unroll
+                        for (int k1 = 0; k1 < N; k1++) {
+                            const double a = fabs(hv[k1]);
+                            if (k1 == 0 && k2 == 0) continue;              // C00 is not scanned
+                            if (k1 == 0 && k2 == 1) a01 = a;
+                            else if (k1 == 0) m0 = fmax(m0, a);
+                            else if (k1 == 1 && k2 == 0) a10 = a;
+                            else mp = fmax(mp, a);
+                        }
+                    }
+                    const double M = fmax(fmax(mp, a10), fmax(m0, a01));
+                    const bool edge = !(mp == M) && (a10 == M || (!(m0 == M) && a01 == M));
+                    if (emits) orow[(long long)(i - (N - 1)) * p.out_stride] = (float)(M * weight(edge, we, wt));
+                }
+            }
+        });
+    };
+
+    issue(0, 0);
+    for (int g = 0; g < ngroups; g += 2) {
+        if (g + 1 < ngroups) issue(g + 1, 1);
+        compute(g, 0);
+        if (g + 1 >= ngroups) break;
+        if (g + 2 < ngroups) issue(g + 2, 0);
+        compute(g + 1, 1);
+    }
+}
+
+template <int N, int BPP>
+hipError_t launch_exact_small(const MapParams& p, hipStream_t s)
+{
+    constexpr int per_wg = (kExST / 64) * (64 - (N - 1));
+    dim3 grid((p.w + per_wg - 1) / per_wg, p.tiles_y);
+    hipLaunchKernelGGL((dcte_exact_small<N, BPP>), grid, dim3(kExST), 0, s, p);
+    return hipGetLastError();
+}
+
 }  // namespace
 
-bool exact_supported(int n, int sem) { return sem == kSemLqr && n == 8; }
-int exact_tile_w(int n) { return n == 8 ? kEx8T : 0; }
+bool exact_supported(int n, int sem) { return sem == kSemLqr && (n == 2 || n == 4 || n == 8 || n == 16); }
+int exact_tile_w(int n)
+{
+    return n == 8 ? kEx8T : (n == 16 ? 64 : (kExST / 64) * (64 - (n - 1)));
+}
 int exact_default_tile_h(int n) { return DCTE_EX_TILE_H; }
 
 hipError_t launch_map_exact(int n, int bpp, int sem, const MapParams& p, hipStream_t s)
@@ -320,6 +788,15 @@ hipError_t launch_map_exact(int n, int bpp, int sem, const MapParams& p, hipStre
     if (n == 8) {
         if (bpp == 1) return launch_exact8<1>(p, s);
         if (bpp == 3) return launch_exact8<3>(p, s);
+    } else if (n == 16) {
+        if (bpp == 1) return launch_exact16<1>(p, s);
+        if (bpp == 3) return launch_exact16<3>(p, s);
+    } else if (n == 4) {
+        if (bpp == 1) return launch_exact_small<4, 1>(p, s);
+        if (bpp == 3) return launch_exact_small<4, 3>(p, s);
+    } else if (n == 2) {
+        if (bpp == 1) return launch_exact_small<2, 1>(p, s);
+        if (bpp == 3) return launch_exact_small<2, 3>(p, s);
     }
     return hipErrorInvalidValue;
 }

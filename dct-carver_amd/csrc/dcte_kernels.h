@@ -32,6 +32,7 @@ struct MapParams {
     float we, wt;            // edges / textures weights, pre-scaled to luma units
     float tie_tau;           // relative edge/texture margin sent to refinement
     float edges, textures;   // raw weights (refinement path)
+    double ct[4];            // makect twiddles (N = 2, 4: the exact kernels)
     // Refinement lists, per 64-column strip s = (by * tiles_x + bx) * SPT +
     // strip in the tile (SPT = TW / 64 at N <= 8, 1 at N = 16): the pixels it
     // flags, as (y - ys) * 64 + (x - strip x0), at fix_list[s * 64 * tile_h ...];
