@@ -53,6 +53,8 @@ def parse(argv=None):
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--no-stress", action="store_true",
                     help="skip the tie-dense (line-art) frame timed after the headline")
+    ap.add_argument("--no-exact", action="store_true",
+                    help="skip the DCTE_OPT_EXACT (bit-identical fp64) map timed after the headline")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: stage halos through host memory (rehearsal of the N>1 path "
                          "on a box with fewer GPUs than ranks)")
@@ -262,6 +264,54 @@ def stress(ctx, n, S, e, t, dev, stream, iters=10, rounds=3):
             "value": round(S * S / best_call / 1e3, 1), "unit": "Mpx/s",
             "what": "after the timed region; map + fp64 tie refinement of the tie-dense frame, "
                     f"best of {rounds} rounds of {iters} device calls (HIP events)"}
+
+
+# fp64 VALU operations per output pixel of the exact kernels (dcte_exact.hip):
+# the reference's own ops (ddct8x8s / ddct16x16s / ddct2d, no FMA), the scan's
+# maxima and the decision per output pixel (idle halo lanes included), counted
+# from the kernels (DESIGN.md §3 "exact map"); the N = 16 figure includes the
+# pass-1 work the eight waves of a column repeat (246 instead of 114 per pixel)
+EXACT_FP64_OPS = {2: 21, 4: 105, 8: 425, 16: 2270}
+# gfx950 fp64 VALU: 16 lanes / clk / SIMD x 1024 SIMDs x 2.4 GHz
+FP64_PEAK_OPS = 256 * 4 * 16 * 2.4e9
+
+
+def exact(n, S, e, t, dev, frame, iters=10, rounds=3):
+    """DCTE_OPT_EXACT on the headline frame, timed after the headline: the map
+    bit-identical to the reference (its fp64 operation order, dcte_exact.hip),
+    HIP events around each launch; best of `rounds` rounds of `iters`."""
+    import torch
+    import dctenergy
+    out = torch.empty((S, S), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    with dctenergy.Context(ngpus=0, exact=True) as cx:
+        def call():
+            cx.energy_map_device(frame.data_ptr(), frame.stride(0), S, S, 3, 0, S, 0, S, n, e, t,
+                                 out.data_ptr(), out.stride(0), stream)
+        for _ in range(2):
+            call()
+        torch.cuda.synchronize()
+        best = 1e9
+        for _ in range(rounds):
+            cx.profile_read()
+            cx.set_option(dctenergy.DCTE_OPT_PROFILE, 1)
+            for _ in range(iters):
+                call()
+            torch.cuda.synchronize()
+            cx.set_option(dctenergy.DCTE_OPT_PROFILE, 0)
+            launches, kms = cx.profile_read()
+            best = min(best, kms / launches)
+    del out
+    ops = EXACT_FP64_OPS[n]
+    rate = S * S * ops / (best * 1e-3)
+    return {"ms": round(best, 4), "value": round(S * S / best / 1e3, 1), "unit": "Mpx/s",
+            "kernel": f"dcte_exact{n if n >= 8 else '_small'}",
+            "fp64": {"ops_per_px": ops, "achieved_tops": round(rate / 1e12, 2),
+                     "peak_tops": round(FP64_PEAK_OPS / 1e12, 2),
+                     "frac": round(rate / FP64_PEAK_OPS, 4)},
+            "what": "DCTE_OPT_EXACT (every pixel bit-identical to the reference's fp64 "
+                    "arithmetic) on the same frame after the timed region; map launches alone, "
+                    f"HIP events, best of {rounds} rounds of {iters}"}
 
 
 def pmc_figures(n, W, px_per_rank):
@@ -597,6 +647,8 @@ def main():
             res["config"]["parallelism"] += f"; {world} ranks share {ndev} GPU(s)"
         if world == 1 and not args.no_stress:
             res["stress"] = stress(ctx, n, S, e, t, dev, stream)
+        if world == 1 and not args.no_exact:
+            res["exact"] = exact(n, S, e, t, dev, buf)
         if world == 1 and not args.no_host_path:
             res["host_path"] = host_path(ctx, buf, n, e, t)
         if world == 1 and not args.no_cpu_baseline:
