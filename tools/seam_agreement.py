@@ -69,7 +69,7 @@ def main():
                         from seam_util import carve
                         host, cpu = img, True
                         for k in range(S):
-                            rs = O.seam_find(O.energy_map(host, n, e, t))
+                            rs = O.seam_find(O.energy_map(host, n, e, t, nthreads=16))
                             cpu = cpu and bool(np.array_equal(rs, cx[k]))
                             host = carve(host, rs)
                     prefix = next((k for k, s in enumerate(same) if not s), S)
