@@ -19,6 +19,7 @@
 #include "../../include/dctenergy.h"
 #include "dcte_kernels.h"
 #include "dcte_luma.h"
+#include "dcte_host.h"
 #include "dcte_norm.h"
 #include "dcte_ref64.h"
 
@@ -212,21 +213,7 @@ int ensure_tiles(dcte_ctx* ctx, FixScratch* f, size_t ntiles)
     return DCTE_OK;
 }
 
-// the reference's makect (src/fft2d/fftsg.c:724-740) for nc = n, with libm,
-// exactly as the reference evaluates it; used by the fp64 refinement
-void small_twiddles(int n, double ct[4])
-{
-    ct[0] = ct[1] = ct[2] = ct[3] = 0.0;
-    if (n != 2 && n != 4) return;
-    int nch = n >> 1;
-    double delta = atan(1.0) / nch;
-    ct[0] = cos(delta * nch);
-    ct[nch] = 0.5 * ct[0];
-    for (int j = 1; j < nch; j++) {
-        ct[j] = 0.5 * cos(delta * j);
-        ct[n - j] = 0.5 * sin(delta * j);
-    }
-}
+using dcte::small_twiddles;
 
 // kernel weights divide by this: hat units of dcte_math.h (C * N for N = 8, 16;
 // C for the unnormalised N = 2, 4) times the luma unit (1/1275000 for liblqr,
@@ -266,6 +253,38 @@ dcte::FixParams fix_params(const uint8_t* px, long long rowstride, int w, int h,
 
 int ensure_buf(dcte_ctx* ctx, void** p, size_t* cap, size_t bytes);
 
+int device_cus(Device& d)
+{
+    if (d.cus <= 0 && hipDeviceGetAttribute(&d.cus, hipDeviceAttributeMultiprocessorCount, d.id) != hipSuccess)
+        d.cus = 256;
+    return d.cus;
+}
+
+// Output rows per map workgroup when DCTE_OPT_TILE_H does not fix them: the
+// shape that finishes first under a rounds model.  A launch of nwg workgroups
+// on `resident` slots takes ceil(nwg / resident) rounds, each as long as one
+// tile: its rows plus a fixed prologue (the N - 1 warm-up rows and the group
+// loop's setup, ~N + 3 rows).  Large frames keep th_max (128 rows: 8 full
+// rounds at 16384^2, N = 8); a 4096^2 frame, whose 128-row tiles filled only
+// half of the slots, gets 64 (one full round); 6000 x 4000 gets 96.  Ties go
+// to the taller tile.
+int pick_tile_h(int n, int rows_a, int rows_b, int tiles_x, long long resident, int th_max)
+{
+    const int w0 = n + 3;
+    int best = th_max;
+    double best_cost = 0.0;
+    for (int th = th_max; th >= 16; th--) {
+        const long long nwg = (long long)tiles_x * ((rows_a + th - 1) / th + (rows_b + th - 1) / th);
+        const long long rounds = (nwg + resident - 1) / resident;
+        const double cost = (double)rounds * (double)(th + w0);
+        if (th == th_max || cost < best_cost * (1.0 - 1e-9)) {
+            best = th;
+            best_cost = cost;
+        }
+    }
+    return best;
+}
+
 // The exact map (DCTE_OPT_EXACT, dcte_exact.hip): one launch of the fp64
 // sliding-window kernel over the same row ranges, no refinement lists.  The
 // arguments were checked by run_device.
@@ -274,7 +293,14 @@ int run_exact(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, i
               float textures, int sem, float* d_out, long long out_stride, hipStream_t s)
 {
     const int rows_a = y1 - y0, rows_b = yb1 - yb0;
-    int tile_h = ctx->tile_h > 0 ? ctx->tile_h : dcte::exact_default_tile_h(n);
+    DCTE_HIP(ctx, hipSetDevice(d.id));
+    int tile_h = ctx->tile_h;
+    if (tile_h <= 0) {
+        const int tw = dcte::exact_tile_w(n);
+        tile_h = pick_tile_h(n, rows_a, rows_b, (w + tw - 1) / tw,
+                             (long long)device_cus(d) * dcte::exact_blocks_per_cu(n, bpp),
+                             dcte::exact_default_tile_h(n));
+    }
     if (tile_h > (rows_a > rows_b ? rows_a : rows_b)) tile_h = rows_a > rows_b ? rows_a : rows_b;
     const int tiles_a = (rows_a + tile_h - 1) / tile_h;
     const int tiles_y = tiles_a + (rows_b + tile_h - 1) / tile_h;
@@ -282,7 +308,6 @@ int run_exact(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, i
         ctx->last_error = "tile rows exceed the launch grid (raise DCTE_OPT_TILE_H)";
         return DCTE_ERANGE;
     }
-    DCTE_HIP(ctx, hipSetDevice(d.id));
     dcte::MapParams p{};
     p.px = static_cast<const uint8_t*>(d_px);
     p.rowstride = rowstride;
@@ -338,12 +363,16 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     DCTE_ARG(ctx, !two || (yb0 >= y1 && yb1 <= h));
     if (!two) yb0 = yb1 = y1;
     if (y1 == y0 && !two) return DCTE_OK;
-    int lo, hi, lo2, hi2;
-    needed_rows(n, sem, h, y1 > y0 ? y0 : yb0, two ? yb1 : y1, lo, hi);
-    DCTE_ARG(ctx, lo >= in_row0 && hi < in_row0 + in_rows);
-    if (two && y1 > y0) {                    // both ranges' rows must be readable
-        needed_rows(n, sem, h, y0, y1, lo2, hi2);
-        DCTE_ARG(ctx, lo2 >= in_row0 && hi2 < in_row0 + in_rows);
+    // every row the clamp reaches for each range must be readable (the rows
+    // between two ranges are never read)
+    int lo, hi;
+    if (y1 > y0) {
+        needed_rows(n, sem, h, y0, y1, lo, hi);
+        DCTE_ARG(ctx, lo >= in_row0 && hi < in_row0 + in_rows);
+    }
+    if (two) {
+        needed_rows(n, sem, h, yb0, yb1, lo, hi);
+        DCTE_ARG(ctx, lo >= in_row0 && hi < in_row0 + in_rows);
     }
     // one buffer resource addresses the readable rows: < 4 GiB
     long long span = (long long)(in_rows - 1) * rowstride + (long long)w * bpp + 3;
@@ -357,12 +386,16 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     const bool exact = ctx->exact && dcte::exact_supported(n, sem);
     if (exact) return run_exact(ctx, d, d_px, rowstride, w, h, bpp, in_row0, in_rows, y0, y1, yb0, yb1, n,
                                 edges, textures, sem, d_out, out_stride, s);
-    int tile_h = ctx->tile_h > 0 ? ctx->tile_h : dcte::map_default_tile_h(n);
+    DCTE_HIP(ctx, hipSetDevice(d.id));
+    int tile_h = ctx->tile_h;
+    if (tile_h <= 0)
+        tile_h = pick_tile_h(n, rows_a, rows_b, dcte::map_tiles_x(n, w),
+                             (long long)device_cus(d) * dcte::map_blocks_per_cu(n, bpp, sem),
+                             dcte::map_default_tile_h(n));
     if (tile_h > (rows_a > rows_b ? rows_a : rows_b)) tile_h = rows_a > rows_b ? rows_a : rows_b;
     if ((long long)tile_h * out_stride * 4 >= (1LL << 31)) return DCTE_ERANGE;
     const int tiles_a = dcte::map_tiles_y(n, rows_a, tile_h);
 
-    DCTE_HIP(ctx, hipSetDevice(d.id));
     // N = 8 launches of at most two rounds of workgroups (a strong-scaling
     // rank's 2048- or 4096-row band): the waves step their priority down
     // through the tile so the workgroups sharing a CU finish together
@@ -372,9 +405,7 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     // vs 87 %, but ran each tile 20 % slower: profiles/r03/band_wide_ab.jsonl.)
     int fair = 0;
     if (n == 8) {
-        if (d.cus <= 0 &&
-            hipDeviceGetAttribute(&d.cus, hipDeviceAttributeMultiprocessorCount, d.id) != hipSuccess)
-            d.cus = 256;
+        device_cus(d);
         const long long nwg = (long long)dcte::map_tiles_x(n, w) *
                               (tiles_a + dcte::map_tiles_y(n, rows_b, tile_h));
         if (nwg <= 2LL * 4 * d.cus) fair = 3;
@@ -1539,35 +1570,6 @@ int dcte_profile_read(dcte_ctx* ctx, long long* launches, double* kernel_ms)
 // fp64 in the reference's operation order (dcte_ref64.h, the same functions
 // the device refinement runs).  No device, no context, no fallback role:
 // the GPU entry points never call these.
-int dcte_energy_window(int n, const double* win, float edges, float textures, float* out)
-{
-    if (!valid_n(n) || !win || !out) return DCTE_EINVAL;
-    double d[16 * 16];
-    memcpy(d, win, sizeof(double) * (size_t)n * (size_t)n);
-    double ct[4];
-    small_twiddles(n, ct);
-    dcte::r64::transform(n, d, ct);
-    *out = dcte::r64::weighted_max(n, d, edges, textures);
-    return DCTE_OK;
-}
-
-int dcte_normalize_u8_host(const float* E, size_t n, int mode, int channels, uint8_t* out)
-{
-    if (!E || !out || n == 0 || !valid_norm(mode, channels)) return DCTE_EINVAL;
-    unsigned kmin = 0xffffffffu, kmax = 0u;
-    for (size_t i = 0; i < n; i++) {
-        const unsigned k = dcte::norm_fkey(E[i]);
-        kmin = k < kmin ? k : kmin;
-        kmax = k > kmax ? k : kmax;
-    }
-    const float mn = dcte::norm_funkey(kmin), mx = dcte::norm_funkey(kmax);
-    for (size_t i = 0; i < n; i++) {
-        const uint8_t v = dcte::norm_one(E[i], mn, mx, mode);
-        for (int c = 0; c < channels; c++) out[i * (size_t)channels + c] = v;
-    }
-    return DCTE_OK;
-}
-
 long long dcte_last_refined(const dcte_ctx* ctx) { return ctx ? ctx->last_refined : 0; }
 
 const char* dcte_strerror(int code)

@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <utility>
 
 #include "dcte_kernels.h"
@@ -773,6 +774,27 @@ hipError_t launch_exact_small(const MapParams& p, hipStream_t s)
 }
 
 }  // namespace
+
+// workgroups of the exact kernel for (n, bpp) one CU holds at once; cached
+int exact_blocks_per_cu(int n, int bpp)
+{
+    static std::atomic<int> cache[4][2];
+    const int ni = n == 2 ? 0 : (n == 4 ? 1 : (n == 8 ? 2 : 3)), bi = bpp == 1 ? 0 : 1;
+    int v = cache[ni][bi].load(std::memory_order_relaxed);
+    if (v) return v;
+    hipError_t e = hipErrorInvalidValue;
+    if (n == 8) e = bpp == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact8<1>, kEx8T, 0)
+                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact8<3>, kEx8T, 0);
+    else if (n == 16) e = bpp == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact16<1>, kEx16T, 0)
+                                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact16<3>, kEx16T, 0);
+    else if (n == 4) e = bpp == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact_small<4, 1>, kExST, 0)
+                                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact_small<4, 3>, kExST, 0);
+    else e = bpp == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact_small<2, 1>, kExST, 0)
+                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact_small<2, 3>, kExST, 0);
+    if (e != hipSuccess || v <= 0) v = 1;
+    cache[ni][bi].store(v, std::memory_order_relaxed);
+    return v;
+}
 
 bool exact_supported(int n, int sem) { return sem == kSemLqr && (n == 2 || n == 4 || n == 8 || n == 16); }
 int exact_tile_w(int n)

@@ -188,6 +188,7 @@ int map_default_tile_h(int n);
 int map_tiles_x(int n, int w);   // map grid (tiles) of a launch
 int map_tiles_y(int n, int rows, int tile_h);
 int map_strips_per_tile(int n);
+int map_blocks_per_cu(int n, int bpp, int sem);   // resident map workgroups per CU (occupancy)
 int dense_batch_entries(int n, int sem);   // entries per dense refinement batch (0: no flat list)
 
 // the exact map (dcte_exact.hip, DCTE_OPT_EXACT): the reference's fp64
@@ -196,5 +197,6 @@ hipError_t launch_map_exact(int n, int bpp, int sem, const MapParams& p, hipStre
 bool exact_supported(int n, int sem);   // else the exact mode refines every pixel of the fp32 map
 int exact_tile_w(int n);                // output columns per workgroup
 int exact_default_tile_h(int n);
+int exact_blocks_per_cu(int n, int bpp);
 
 }  // namespace dcte

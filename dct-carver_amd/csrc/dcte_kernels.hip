@@ -2296,6 +2296,37 @@ int map_tiles_x(int n, int w) { return (w + map_tile_w(n) - 1) / map_tile_w(n); 
 int map_tiles_y(int n, int rows, int tile_h) { return (rows + tile_h - 1) / tile_h; }
 int map_strips_per_tile(int n) { return n == 16 ? 1 : map_tile_w(n) / 64; }
 
+// workgroups of dcte_map<N, BPP, SEM> one CU holds at once (the launch-shape
+// model of the host, dcte_capi.cpp pick_tile_h); cached per instantiation
+template <int N, int BPP, int SEM>
+static int map_blocks_per_cu_t()
+{
+    static std::atomic<int> cache{0};
+    int v = cache.load(std::memory_order_relaxed);
+    if (!v) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_map<N, BPP, SEM>, Geo<N, SEM>::T, 0) != hipSuccess || v <= 0)
+            v = 1;
+        cache.store(v, std::memory_order_relaxed);
+    }
+    return v;
+}
+template <int N>
+static int map_blocks_per_cu_n(int bpp, int sem)
+{
+    if (sem == kSemLqr) return bpp == 1 ? map_blocks_per_cu_t<N, 1, kSemLqr>() : map_blocks_per_cu_t<N, 3, kSemLqr>();
+    if (bpp == 1) return map_blocks_per_cu_t<N, 1, kSemPreview>();
+    return bpp == 3 ? map_blocks_per_cu_t<N, 3, kSemPreview>() : map_blocks_per_cu_t<N, 4, kSemPreview>();
+}
+int map_blocks_per_cu(int n, int bpp, int sem)
+{
+    switch (n) {
+    case 2: return map_blocks_per_cu_n<2>(bpp, sem);
+    case 4: return map_blocks_per_cu_n<4>(bpp, sem);
+    case 8: return map_blocks_per_cu_n<8>(bpp, sem);
+    default: return map_blocks_per_cu_n<16>(bpp, sem);
+    }
+}
+
 template <int N, int BPP, int SEM>
 static hipError_t launch_map_t(const MapParams& p, hipStream_t s)
 {

@@ -5,6 +5,7 @@
 #include "dcte_plugin.h"
 
 #include <math.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -135,19 +136,20 @@ int dcte_plugin_lookup(const dcte_map_cache *c, int x, int y, int w, int h, int 
  * 0.2126 * (R / 255) etc., added in the formula's order -- bit-identical to
  * evaluating it per pixel. */
 static double g_luma_tab[4][256];
-static int g_luma_tab_ready;
+static pthread_once_t g_luma_once = PTHREAD_ONCE_INIT;
 
-static void luma_tables(void)
+static void fill_luma_tables(void)
 {
-    if (g_luma_tab_ready) return;
     for (int v = 0; v < 256; v++) {
         g_luma_tab[0][v] = (double)v / 255;
         g_luma_tab[1][v] = 0.2126 * ((double)v / 255);
         g_luma_tab[2][v] = 0.7152 * ((double)v / 255);
         g_luma_tab[3][v] = 0.0722 * ((double)v / 255);
     }
-    g_luma_tab_ready = 1;
 }
+
+/* filled once per process, whichever thread's callback comes first */
+static void luma_tables(void) { pthread_once(&g_luma_once, fill_luma_tables); }
 
 static double lqr_luma(const unsigned char *q, int bpp)
 {
@@ -202,6 +204,14 @@ int dcte_plugin_window_check(dcte_map_cache *c, int x, int y, int w, int h,
     return 1;
 }
 
+static void reset_checked(dcte_map_cache *c)
+{
+    for (int i = 0; i < c->mh; i++) {
+        c->ver_lo[i] = 1;
+        c->ver_hi[i] = 0;
+    }
+}
+
 int dcte_plugin_lookup_hook(dcte_map_cache *c, int x, int y, int w, int h, int orientation,
                             dcte_rwindow_read_fn rd, void *rw, float *out)
 {
@@ -218,11 +228,13 @@ int dcte_plugin_lookup_hook(dcte_map_cache *c, int x, int y, int w, int h, int o
         c->mw--;
         c->steps++;
         c->band_valid = 1;
-        for (int i = 0; i < c->mh; i++) {          /* nothing of the new band checked yet */
-            c->ver_lo[i] = 1;
-            c->ver_hi[i] = 0;
-        }
+        reset_checked(c);                          /* nothing of the new band checked yet */
     }
+    /* liblqr walks a pass (an update or a rebuild of its energy map) in
+     * increasing rows: a callback above the previous one starts another pass,
+     * and liblqr's image may have changed since the columns were checked */
+    if (y < c->last_y) reset_checked(c);
+    c->last_y = y;
     const int chk = dcte_plugin_window_check(c, x, y, w, h, rd, rw);
     const int k = chk == 1 ? x - c->band_x0[y] : -1;
     if (chk <= 0 || k < 0 || k >= c->bw) {

@@ -43,7 +43,8 @@ typedef struct {
     int *band_x0;          /* mh: first band column per row */
     float *band_e;         /* mh x bw energies of the last step's band */
     unsigned char *band_px;/* mh x bw x bpp pixels of the carved frame (window check) */
-    int *ver_lo, *ver_hi;  /* mh: columns of each row already checked against liblqr this step */
+    int *ver_lo, *ver_hi;  /* mh: columns of each row already checked against liblqr this pass */
+    int last_y;            /* row of the previous hooked callback: a lower one starts a new pass */
     long long served_band, missed, out_of_band, steps, reads;
 } dcte_map_cache;
 

@@ -172,7 +172,9 @@ int dcte_energy_map_device(dcte_ctx *ctx, int device, const void *d_px,
  * launch: [y0, y1) and [yb0, yb1) with y1 <= yb0 (yb0 == yb1: the second is
  * empty); row y of either at d_out + (y - y0) * out_stride.  For a row-band
  * shard: both halo-dependent edge ranges of a band after the
- * RCCL halo exchange (the rows the clamp reaches for BOTH ranges readable). */
+ * RCCL halo exchange.  The rows the clamp reaches for each range must be
+ * readable; rows between the two ranges' needs are never read (they only
+ * have to lie inside the [in_row0, in_row0 + in_rows) span). */
 int dcte_energy_map_device2(dcte_ctx *ctx, int device, const void *d_px,
                             long long rowstride, int w, int h, int bpp,
                             int in_row0, int in_rows, int y0, int y1, int yb0, int yb1,

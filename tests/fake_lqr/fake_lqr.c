@@ -395,7 +395,11 @@ int fake_window_check_selftest(int n, int bpp, unsigned seed)
  * mirror's rules; 1 = after the build liblqr's image differs slightly from
  * the frame the plug-in was given (+1e-3 luma); 2 = every seam liblqr carves
  * is shifted by one column in one row; 3 = liblqr's DP takes the rightmost
- * minimum on ties (seam_find_rightmost).  verify: re-run the original body on
+ * minimum on ties (seam_find_rightmost); 4 = after the first seam's update
+ * liblqr's image changes (up to 1e-3 luma, varying along the row, so the AC
+ * content changes) and it runs that update pass again at the SAME width (a
+ * second callback pass over the same pixels, from row 0).
+ * verify: re-run the original body on
  * every hook-served callback and count values off the parity tolerance. */
 int fake_resize(const uint8_t *px, int w, int h, int bpp, int n, float edges, float textures,
                 int use_gpu, int hook, int seams, int transposed, int diverge, int verify,
@@ -479,6 +483,16 @@ int fake_resize(const uint8_t *px, int w, int h, int bpp, int n, float edges, fl
             }
         clock_gettime(CLOCK_MONOTONIC, &t1);
         update_ns += (t1.tv_sec - t0.tv_sec) * 1000000000LL + (t1.tv_nsec - t0.tv_nsec);
+        if (diverge == 4 && k == 0) {
+            for (size_t i = 0; i < (size_t)cw * fh; i++) luma[i] += 1e-3 * (double)(i % 7) / 7.0;
+            for (int y = 0; y < fh; y++)
+                for (int x = xmin[y]; x <= xmax[y]; x++) {
+                    rw.x = x;
+                    rw.y = y;
+                    emap[(size_t)y * cw + x] = dct_pixel_energy(x, y, cw, fh, &rw, &p);
+                    calls++;
+                }
+        }
     }
     memcpy(out_emap, emap, sizeof(float) * (size_t)cw * fh);
     if (out_px) memcpy(out_px, img, (size_t)cw * fh * bpp);

@@ -42,6 +42,7 @@ KNOBS = {
     "DCTE_MEMO_SLOTS": ("dcte_kernels.hip", "64"),
     "DCTE_EX_TILE_H": ("dcte_exact.hip", "64"),
     "DCTE_EX_MINW": ("dcte_exact.hip", "1"),
+    "DCTE_EX16_MINW": ("dcte_exact.hip", "2"),
     "DCTE_SHIFT_VEC": ("dcte_seam.hip", "1"),
     "DCTE_DP_C": ("dcte_dp.hip", "1"),
     "DCTE_DP_R": ("dcte_dp.hip", "16"),

@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "dct-carver_amd")]
 
 
-def load(path, exact=False):
+def load(path, exact=False, tile_h=0):
     L = ctypes.CDLL(path)
     vp = ctypes.c_void_p
     L.dcte_create.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_uint]
@@ -31,6 +31,8 @@ def load(path, exact=False):
     L.dcte_set_option(h, 2, 1.0)
     if exact:
         assert L.dcte_set_option(h, 10, 1.0) == 0          # DCTE_OPT_EXACT
+    if tile_h:
+        assert L.dcte_set_option(h, 4, float(tile_h)) == 0  # DCTE_OPT_TILE_H
     return L, h
 
 
@@ -49,23 +51,29 @@ def main():
                     help="also map a CHECKxCHECK natural frame and a dots-on-flat frame with "
                          "every build and compare with the CPU oracle (tolerance, class flips)")
     ap.add_argument("--exact", action="store_true", help="DCTE_OPT_EXACT (the fp64 map)")
+    ap.add_argument("--width", type=int, default=0, help="frame width (default --size)")
+    ap.add_argument("--height", type=int, default=0, help="frame height (default --size)")
+    ap.add_argument("--tile-h", default="0",
+                    help="comma-separated DCTE_OPT_TILE_H values, each a separate entry per lib (0: the launcher's pick)")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     import torch
     from dctenergy import synth
     S = a.size
-    frame = synth.natural_rows(0, S, S, a.bpp, seed=0, device="cuda")
-    out = torch.empty((S, S), dtype=torch.float32, device="cuda")
+    W, H = a.width or S, a.height or S
+    frame = synth.natural_rows(0, H, W, a.bpp, seed=0, device="cuda")
+    out = torch.empty((H, W), dtype=torch.float32, device="cuda")
     ref = None
-    libs = [(p, *load(p, a.exact)) for p in a.libs]
+    ths = [int(v) for v in a.tile_h.split(",")]
+    libs = [(f"{p}@th{th}" if len(ths) > 1 else p, *load(p, a.exact, th)) for p in a.libs for th in ths]
     stream = torch.cuda.current_stream().cuda_stream
-    times = {p: [] for p in a.libs}
+    times = {p[0]: [] for p in libs}
     same = {}
     for r in range(a.rounds):
         for p, L, h in libs:
             def call():
-                rc = L.dcte_energy_map_device(h, 0, frame.data_ptr(), frame.stride(0), S, S, a.bpp, 0, S,
-                                              0, S, a.n, 0.3, 0.7, a.sem, out.data_ptr(), out.stride(0), stream)
+                rc = L.dcte_energy_map_device(h, 0, frame.data_ptr(), frame.stride(0), W, H, a.bpp, 0, H,
+                                              0, H, a.n, 0.3, 0.7, a.sem, out.data_ptr(), out.stride(0), stream)
                 assert rc == 0, rc
             n = ctypes.c_longlong()
             ms = ctypes.c_double()
@@ -119,11 +127,11 @@ def main():
                 # a class flip changes the weight: e = 0.3 vs t = 0.7 differ by > 2x
                 flips += int((np.abs(got - ref) > 0.25 * np.abs(ref)).sum())
             checks[p] = {"check_off_tol": bad, "check_flips": flips, "check_max_rel": worst}
-    for p in a.libs:
+    for p, _, _ in libs:
         t = times[p]
-        print(json.dumps({"lib": os.path.basename(p), "n": a.n, "size": S, "e2e": a.e2e, "exact": a.exact,
+        print(json.dumps({"lib": os.path.basename(p), "n": a.n, "size": S, "w": W, "h": H, "e2e": a.e2e, "exact": a.exact,
                           "median_ms": round(statistics.median(t), 4), "min_ms": round(min(t), 4),
-                          "mpx_s": round(S * S / statistics.median(t) / 1e3, 1),
+                          "mpx_s": round(W * H / statistics.median(t) / 1e3, 1),
                           "bit_equal_first": same[p], **checks.get(p, {})}))
 
 
