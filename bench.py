@@ -414,6 +414,7 @@ def main():
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     gloo = args.dist_backend == "gloo"
+    rccl_log = D.rccl_log_setup("dcte-bench") if world > 1 and not gloo else None
     if world > 1:
         if gloo:
             dist.init_process_group("gloo")
@@ -518,7 +519,11 @@ def main():
     ctx.set_option(dctenergy.DCTE_OPT_PROFILE, 0)
     stats = torch.tensor([elapsed, kern_ms / args.steps, enqueued], dtype=torch.float64,
                          device="cpu" if gloo else dev)
+    per_rank_kernel_ms = [kern_ms / args.steps]
     if world > 1:
+        everyone = [torch.zeros_like(stats) for _ in range(world)]
+        dist.all_gather(everyone, stats)
+        per_rank_kernel_ms = [round(float(v[1]), 4) for v in everyone]
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
     elapsed = float(stats[0])
     kernel_ms_max_rank = float(stats[1])
@@ -554,6 +559,38 @@ def main():
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         check = bool(ok.item())
         del ref_in, ref_out
+
+    # the halo exchange alone (after the metric's region): one exchange per
+    # step, timed over `reps` exchanges on their own, max over ranks; and which
+    # RCCL transport carried them (the ranks' RCCL INFO logs)
+    exchange = None
+    if world > 1 and not gloo:
+        reps = 20
+        for r in D.exchange_halos(buf, band):
+            r.wait()
+        torch.cuda.synchronize()
+        dist.barrier()
+        x0 = time.perf_counter()
+        for _ in range(reps):
+            for r in D.exchange_halos(buf, band):
+                r.wait()
+        torch.cuda.synchronize()
+        xms = torch.tensor([(time.perf_counter() - x0) * 1e3 / reps], dtype=torch.float64, device=dev)
+        dist.all_reduce(xms, op=dist.ReduceOp.MAX)
+        summ = (D.transport_summary(rccl_log, rank) if rccl_log
+                else {"error": "RCCL's log routed by the caller (NCCL_DEBUG_FILE / INFO or TRACE)"})
+        gathered = [None] * world
+        dist.all_gather_object(gathered, summ)
+        halo_bytes = (band.hl + band.hr) * W * 3
+        exchange = {"ms_per_exchange": round(float(xms.item()), 4),
+                    "halo_bytes_per_rank": halo_bytes,
+                    "transport_per_rank": [g.get("transports") for g in gathered],
+                    "transport_errors": sorted({g["error"] for g in gathered if g.get("error")}) or None,
+                    "rccl_version": gathered[0].get("version"),
+                    "connections_rank0": gathered[0].get("connections"),
+                    "what": f"{reps} halo exchanges alone (batch_isend_irecv of N/2-1 + N/2 rows "
+                            "each way), after the timed region, max over ranks; transports "
+                            "parsed from each rank's RCCL INFO log (NCCL_DEBUG_FILE)"}
 
     # end to end: the step plus the gather of every band's
     # map to rank 0 over RCCL, reported beside the kernel-only metric
@@ -638,6 +675,10 @@ def main():
             res["check_bands_bit_exact"] = check
         if e2e is not None:
             res["end_to_end"] = e2e
+        if world > 1:
+            res["per_rank_kernel_ms"] = per_rank_kernel_ms
+        if exchange is not None:
+            res["halo_exchange"] = exchange
         if world > 1 and gloo:
             res["config"]["parallelism"] += " (halo via gloo rehearsal)"
         if world > 1 and not gloo and args.shared_gpu:

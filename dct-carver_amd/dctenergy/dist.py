@@ -76,6 +76,54 @@ def make_band(H, rank, world, n, rows_per_rank=None):
     return band
 
 
+def rccl_log_setup(tag="dcte"):
+    """Before init_process_group (backend "nccl" = RCCL): have RCCL write its
+    INFO log (connection set-up included) to a per-process file, so the run
+    can report which transport actually carried the halos
+    (transport_summary).  A level the caller set below INFO (unset, VERSION,
+    WARN -- the GPU boxes export NCCL_DEBUG=VERSION) is raised to INFO; the
+    log goes to the file, not to the caller's streams.  Returns the file path,
+    or None when the caller already routes RCCL's log (NCCL_DEBUG_FILE) or
+    asked for more than INFO."""
+    import os
+    import tempfile
+    level = os.environ.get("NCCL_DEBUG", "").upper()
+    if os.environ.get("NCCL_DEBUG_FILE") or level in ("INFO", "TRACE"):
+        return None
+    path = os.path.join(tempfile.gettempdir(), f"{tag}.rccl.{os.getpid()}.log")
+    os.environ["NCCL_DEBUG"] = "INFO"
+    os.environ["NCCL_DEBUG_SUBSYS"] = "INIT,P2P,NET"
+    os.environ["NCCL_DEBUG_FILE"] = path
+    return path
+
+
+def transport_summary(path, rank=None):
+    """What RCCL's INFO log says about this rank's connections: every
+    "a[..] -> b[..] via TRANSPORT" line, counted per (peer, transport) -- e.g.
+    P2P/IPC (xGMI peer-to-peer), SHM, NET/Socket (the one-GPU rehearsal's
+    loopback) -- and the RCCL version line."""
+    import re
+    out = {"connections": {}, "version": None, "log": path}
+    try:
+        with open(path, errors="replace") as f:
+            text = f.read()
+    except OSError:
+        out["error"] = "no RCCL log"
+        return out
+    m = re.search(r"(?:RCCL|NCCL) version ([\w.+-]+)", text)
+    out["version"] = m.group(1) if m else None
+    pat = re.compile(r"(\d+)\[[^\]]*\] -> (\d+)\[[^\]]*\][^\n]*? via ([^\s,]+)")
+    conns = {}
+    for a, b, via in pat.findall(text):
+        if rank is not None and int(a) != rank and int(b) != rank:
+            continue
+        key = f"{a}->{b} {via}"
+        conns[key] = conns.get(key, 0) + 1
+    out["connections"] = conns
+    out["transports"] = sorted({k.split(" ", 1)[1] for k in conns})
+    return out
+
+
 def halo_ops(buf, band, group=None):
     """P2P ops that fill `buf`'s halo rows from the neighbour ranks and send
     this rank's edge rows to them (buf: [band.rows, ...] contiguous tensor).

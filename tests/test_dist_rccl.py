@@ -83,3 +83,11 @@ def test_config4_bench_eight_ranks_on_one_gpu():
     assert res["check_bands_bit_exact"] is True
     assert res["end_to_end"]["gather_ms"] > 0
     assert res["value"] > 0 and res["roofline"]["launches_timed"] > 0
+    # self-describing N > 1 lines: which RCCL transport carried the halos (here
+    # the socket transport of the one-GPU rehearsal), each rank's kernel time,
+    # the exchange time per step
+    assert len(res["per_rank_kernel_ms"]) == 8 and min(res["per_rank_kernel_ms"]) > 0
+    x = res["halo_exchange"]
+    assert x["ms_per_exchange"] > 0 and x["halo_bytes_per_rank"] == (3 + 4) * 16384 * 3
+    assert len(x["transport_per_rank"]) == 8 and all(x["transport_per_rank"]), x
+    assert any("NET" in t for t in x["transport_per_rank"][0]), x
