@@ -110,7 +110,7 @@ def transport_summary(path, rank=None):
     except OSError:
         out["error"] = "no RCCL log"
         return out
-    m = re.search(r"(?:RCCL|NCCL) version ([\w.+-]+)", text)
+    m = re.search(r"(?:RCCL|NCCL) version[ :]*([\w.+-]+)", text)
     out["version"] = m.group(1) if m else None
     pat = re.compile(r"(\d+)\[[^\]]*\] -> (\d+)\[[^\]]*\][^\n]*? via ([^\s,]+)")
     conns = {}
