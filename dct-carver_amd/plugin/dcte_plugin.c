@@ -55,6 +55,9 @@ int dcte_plugin_build_ex(dcte_map_cache *c, const uint8_t *px, int w, int h, int
     dcte_ctx *ctx = plugin_ctx();
     if (!ctx) return c->status = g_ctx_status;
     if (w <= 0 || h <= 0) return c->status = DCTE_EINVAL;
+    /* the process-wide context follows the latest build's mode */
+    if (dcte_set_option(ctx, DCTE_OPT_EXACT, (flags & DCTE_PLUGIN_EXACT) ? 1.0 : 0.0) != DCTE_OK)
+        return c->status = DCTE_EINVAL;
     c->map = (float *)malloc(sizeof(float) * (size_t)w * (size_t)h);
     if (!c->map) return c->status = DCTE_ENOMEM;
     const int ho = with_transposed ? 1 : 0;

@@ -49,6 +49,10 @@ typedef struct {
 } dcte_map_cache;
 
 #define DCTE_PLUGIN_SEAM_HOOK 1u
+/* every energy the plug-in serves is the reference's own double: the maps and
+ * the hook's band updates in the exact mode (DCTE_OPT_EXACT), so liblqr carves
+ * the reference's seams */
+#define DCTE_PLUGIN_EXACT 2u
 
 /* Build the map(s) for the frame handed to lqr_carver_new (src/render.c:312):
  * orientation 0 always, and the transposed frame's map too when
@@ -63,7 +67,10 @@ int dcte_plugin_build(dcte_map_cache *c, const uint8_t *px, int w, int h, int bp
 /* dcte_plugin_build with flags: DCTE_PLUGIN_SEAM_HOOK also sets up the
  * device mirror of the carver for the orientation liblqr will resize in
  * (with_transposed: vertical, 1; else 0).  Without a GPU, or when the mirror
- * cannot be set up, the build behaves as dcte_plugin_build. */
+ * cannot be set up, the build behaves as dcte_plugin_build.
+ * DCTE_PLUGIN_EXACT: the maps and the mirror's band updates are computed in
+ * the reference's fp64 arithmetic (bit-identical to the original callback);
+ * without it they agree with it within 1e-5 relative. */
 int dcte_plugin_build_ex(dcte_map_cache *c, const uint8_t *px, int w, int h, int bpp,
                          size_t rowstride, int blocksize, float edges, float textures,
                          int with_transposed, unsigned flags);

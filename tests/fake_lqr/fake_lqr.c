@@ -401,6 +401,10 @@ int fake_window_check_selftest(int n, int bpp, unsigned seed)
  * second callback pass over the same pixels, from row 0).
  * verify: re-run the original body on
  * every hook-served callback and count values off the parity tolerance. */
+/* extra plug-in build flags for fake_resize (DCTE_PLUGIN_EXACT) */
+static unsigned g_extra_flags;
+void fake_set_plugin_flags(unsigned flags) { g_extra_flags = flags; }
+
 int fake_resize(const uint8_t *px, int w, int h, int bpp, int n, float edges, float textures,
                 int use_gpu, int hook, int seams, int transposed, int diverge, int verify,
                 float *out_emap, uint8_t *out_px, int *out_seams, long long *counts, int *gpu_status)
@@ -423,7 +427,7 @@ int fake_resize(const uint8_t *px, int w, int h, int bpp, int n, float edges, fl
     EnergyParameters p;
     params_init(&p, edges, textures, n);
     *gpu_status = use_gpu ? dcte_plugin_build_ex(&p.gpu, px, w, h, bpp, (size_t)w * bpp, n, edges,
-                                                 textures, transposed, hook ? DCTE_PLUGIN_SEAM_HOOK : 0u)
+                                                 textures, transposed, (hook ? DCTE_PLUGIN_SEAM_HOOK : 0u) | g_extra_flags)
                           : DCTE_ENODEV;
     g_fallback_calls = g_served_map = g_verified = g_bad = 0;
     g_orientation = transposed;

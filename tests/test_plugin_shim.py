@@ -42,6 +42,8 @@ def fake():
                                   ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                   ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                   ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_int)]
+        L.fake_set_plugin_flags.restype = None
+        L.fake_set_plugin_flags.argtypes = [ctypes.c_uint]
         L.fake_window_check_selftest.restype = ctypes.c_int
         L.fake_window_check_selftest.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint]
         _lib = L
@@ -273,3 +275,26 @@ def test_carver_mirror_band_is_the_map_of_the_carved_frame(n, transposed):
                 assert np.array_equal(e[y], E[y, cols])
                 assert np.array_equal(bpx[y], px[y, cols])
         c.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,transposed", [(8, False), (16, False), (4, True)])
+def test_exact_plugin_resize_is_the_reference(n, transposed):
+    """DCTE_PLUGIN_EXACT: every value liblqr receives --
+    the build from the exact map, each update from the hook's exact band --
+    is the reference's own; the resize loop then carves the CPU reference
+    loop's seams and ends with exactly the reference map of its image."""
+    img = load_input("wilber_rgb_74x59.npy")
+    fake().fake_set_plugin_flags(2)               # DCTE_PLUGIN_EXACT
+    try:
+        d = resize(img, n, 0.3, 0.7, 8, use_gpu=True, hook=True, transposed=transposed)
+    finally:
+        fake().fake_set_plugin_flags(0)
+    assert d["status"] == dctenergy.DCTE_OK
+    assert d["served_map"] + d["served_band"] > 0.9 * d["callbacks"]
+    host = np.ascontiguousarray(np.swapaxes(img, 0, 1)) if transposed else img
+    for k in range(8):
+        ref_seam = O.seam_find(O.energy_map(host, n, 0.3, 0.7))
+        assert np.array_equal(d["seams"][k], ref_seam), f"seam {k}"
+        host = np.stack([np.delete(host[y], ref_seam[y], axis=0) for y in range(host.shape[0])])
+    assert np.array_equal(d["emap"], O.energy_map(d["px"], n, 0.3, 0.7))
