@@ -784,7 +784,7 @@ int exact_blocks_per_cu(int n, int bpp)
     if (v) return v;
     hipError_t e = hipErrorInvalidValue;
     if (n == 8) e = bpp == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact8<1>, kEx8T, 0)
-                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact8<3>, kEx8T, 0);
+                                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact8<3>, kEx8T, 0);
     else if (n == 16) e = bpp == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact16<1>, kEx16T, 0)
                                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact16<3>, kEx16T, 0);
     else if (n == 4) e = bpp == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact_small<4, 1>, kExST, 0)

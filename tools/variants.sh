@@ -14,6 +14,9 @@ build() {  # name extra-flags...
     $HIPCC $BASE "$@" -c -o $o $src
     objs="$objs $o"
   done
+  local ho=build/variants/$name.dcte_host.o
+  g++ -O3 -std=c++17 -ffp-contract=off -fPIC -c -o $ho csrc/dcte_host.cpp
+  objs="$objs $ho"
   $HIPCC --offload-arch=gfx950 -shared -o build/variants/$name.so $objs
   rm -f $objs
   echo built $name
