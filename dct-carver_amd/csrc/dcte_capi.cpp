@@ -113,7 +113,7 @@ struct dcte_ctx {
     std::vector<Device> devs;
     double tie_tau = kDefaultTieTau;
     bool profile = false;
-    double pin_mib = 64.0;          // DCTE_OPT_PIN_HOST
+    double pin_mib = 1.0;           // DCTE_OPT_PIN_HOST (64 before r05: 4096^2 2.44 -> 1.67 ms at 1)
     int tile_h = 0;                 // DCTE_OPT_TILE_H (0: the kernel's default)
     bool dp_bandwise = false;       // DCTE_OPT_DP_BANDWISE
     unsigned dp_spin_limit = 0;     // DCTE_OPT_DP_SPIN_LIMIT (0: the kernel's default)
@@ -633,7 +633,11 @@ int map_bands(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t ro
                                              hipMemcpyDeviceToHost, d.stream));
             continue;
         }
-        int nch = (y1 - y0 + kChunkRows - 1) / kChunkRows;
+        // at least 8 chunks of >= 256 rows where the band allows (a shorter
+        // first upload and last download: the pipeline's ramp)
+        int crows = (y1 - y0) / 8;
+        crows = crows < 256 ? 256 : (crows > kChunkRows ? kChunkRows : crows);
+        int nch = (y1 - y0 + crows - 1) / crows;
         nch = nch < 1 ? 1 : (nch > kMaxChunks ? kMaxChunks : nch);
         rc = ensure_pipe(ctx, d, 2 * (size_t)nch);
         if (rc) return rc;

@@ -74,7 +74,7 @@ extern "C" {
                               events on its stream (dcte_profile_read) */
 #define DCTE_OPT_PIN_HOST 3 /* host entry points: page-lock the caller's frame
                                and output for the duration of a call when they
-                               are at least this many MiB (default 64; 0 = never),
+                               are at least this many MiB (default 1; 0 = never),
                                so the chunked H2D / D2H copies overlap (pageable
                                copies are staged serially by the runtime) */
 #define DCTE_OPT_TILE_H 4   /* output rows per map workgroup (0 = the kernel's

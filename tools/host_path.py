@@ -17,6 +17,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "dct-carver_amd")]
 
 
+DEFAULT_PIN_MIB = 1.0     # DCTE_OPT_PIN_HOST's default (dcte_capi.cpp)
+
+
 def timed(fn, iters):
     fn()
     ts = []
@@ -54,17 +57,20 @@ def main():
     res = []
     with dctenergy.Context(ngpus=1) as ctx:
         cases = (("pageable, DCTE_OPT_PIN_HOST=0 (runtime-staged copies)", px_np, out_np, 0),
-                 ("pageable, page-locked per call (default)", px_np, out_np, 64),
+                 ("pageable, page-locked per call (default)", px_np, out_np, -1),
+                 ("pageable, page-locked per call from 1 MiB", px_np, out_np, 1),
+                 ("pageable, page-locked per call from 64 MiB", px_np, out_np, 64),
                  ("caller-pinned buffers", px_pin.numpy(), out_pin.numpy(), 64))
         if a.quick:
             cases = cases[1:2]
         for name, src, dst, pin in cases:
-            ctx.set_option(dctenergy.DCTE_OPT_PIN_HOST, pin)
+            # pin < 0: the library's default threshold (a fresh context)
+            ctx.set_option(dctenergy.DCTE_OPT_PIN_HOST, pin if pin >= 0 else DEFAULT_PIN_MIB)
             med, best = timed(lambda: ctx.energy_map(src, a.n, 0.3, 0.7, out=dst), a.iters)
             res.append({"case": f"dcte_energy_map host->host ({name})", "lib": os.path.basename(dctenergy.LIB_PATH),
                         "ms": round(med * 1e3, 2),
                         "best_ms": round(best * 1e3, 2), "mpx_s": round(mpx / med, 1)})
-        ctx.set_option(dctenergy.DCTE_OPT_PIN_HOST, 64)
+        ctx.set_option(dctenergy.DCTE_OPT_PIN_HOST, DEFAULT_PIN_MIB)
         if a.quick:
             for r in res:
                 r.update({"size": S, "n": a.n})
@@ -90,6 +96,20 @@ def main():
             torch.cuda.synchronize()
         med, _ = timed(run, a.iters)
         res.append({"case": name, "ms": round(med * 1e3, 2), "GB_s": round(nbytes / med / 1e9, 2)})
+    # the host path's floor: the frame's H2D and the map's D2H at the same
+    # time on two streams (pinned buffers) -- what the chunk pipeline overlaps
+    s_up, s_down = torch.cuda.Stream(), torch.cuda.Stream()
+    d_px = torch.empty_like(dev)
+
+    def duplex():
+        with torch.cuda.stream(s_up):
+            d_px.copy_(px_pin, non_blocking=True)
+        with torch.cuda.stream(s_down):
+            out_pin.copy_(d_out, non_blocking=True)
+        torch.cuda.synchronize()
+    med, _ = timed(duplex, a.iters)
+    res.append({"case": "H2D frame + D2H map concurrently (pinned, two streams)", "ms": round(med * 1e3, 2),
+                "GB_s": round((px_np.nbytes + out_np.nbytes) / med / 1e9, 2)})
     for r in res:
         r.update({"size": S, "n": a.n})
         print(json.dumps(r), flush=True)
