@@ -486,10 +486,14 @@ def main():
         for a, b in (eds if len(eds) == 1 else []):
             run_rows(a, b, st)
 
-    # halo-dependent edge rows on a stream of their own: they wait for the
-    # halos only, so they run beside the interior instead of after it
-    # (tools/band_split.py: 8 -> 2 us of split overhead per 2048-row band)
-    edge_stream = torch.cuda.Stream(dev) if world > 1 and not gloo else None
+    # The halo-dependent edge rows go AFTER the interior on the same stream,
+    # which waits for the halos only then (they have long landed: the
+    # exchange overlaps the 2041-row interior).  A stream of their own, beside
+    # the interior, was the r02-r04 choice; with the edges in ONE two-range
+    # launch the sequential order costs less: 1.034x vs 1.052x the one-launch
+    # band at N = 8, 1.023x vs 1.037x at N = 16 (tools/band_bench.py,
+    # profiles/r05/band_split_ab.jsonl)
+    rccl_path = world > 1 and not gloo
 
     host_buf = torch.empty(buf.shape, dtype=torch.uint8, pin_memory=True) if world > 1 and gloo else None
 
@@ -508,14 +512,12 @@ def main():
             if band.bot:
                 buf[band.rows - band.bot:].copy_(host_buf[band.rows - band.bot:], non_blocking=True)
             run_edges()
-        elif edge_stream is not None:
+        elif rccl_path:
             reqs = D.exchange_halos(buf, band)   # after this rank's previous step (incl. its edges)
             run_rows(i0, i1)                     # overlaps the exchange
-            with torch.cuda.stream(edge_stream):
-                for r in reqs:
-                    r.wait()                     # the edge stream waits for the halos
-                run_edges(edge_stream.cuda_stream)
-            torch.cuda.current_stream(dev).wait_stream(edge_stream)
+            for r in reqs:
+                r.wait()                         # the stream waits for the halos, then the edges
+            run_edges()
         else:
             run_rows(i0, i1)
             run_edges()
