@@ -539,16 +539,17 @@ bool valid_norm(int mode, int channels)
 // Page-locks a caller buffer for the duration of a host call (RAII).  A
 // buffer that is already pinned, or that the runtime refuses, stays as it is:
 // pinning only lets the chunk copies overlap, it never changes results.
+// The range registered is exactly the caller's bytes: a page-rounded range
+// makes the runtime reject (invalid argument) a copy to a neighbouring buffer
+// that shares the first or last page -- the output array numpy allocates
+// right after the frame, say (tools/pin_probe.cpp, profiles/r05/pin_probe.txt).
 struct HostPin {
     void* base = nullptr;
     HostPin(const dcte_ctx* ctx, const void* p, size_t bytes)
     {
         if (ctx->pin_mib <= 0 || (double)bytes < ctx->pin_mib * 1048576.0) return;
-        const uintptr_t pg = 4096;
-        uintptr_t a = reinterpret_cast<uintptr_t>(p) & ~(pg - 1);
-        uintptr_t b = (reinterpret_cast<uintptr_t>(p) + bytes + pg - 1) & ~(pg - 1);
-        void* v = reinterpret_cast<void*>(a);
-        if (hipHostRegister(v, b - a, hipHostRegisterDefault) == hipSuccess) base = v;
+        void* v = const_cast<void*>(p);
+        if (hipHostRegister(v, bytes, hipHostRegisterDefault) == hipSuccess) base = v;
         else (void)hipGetLastError();
     }
     ~HostPin()

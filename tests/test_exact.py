@@ -237,3 +237,34 @@ def test_exact_off_again_is_the_fast_map(ex):
         assert np.array_equal(ex.energy_map(img, 8, 0.3, 0.7), f)
     finally:
         ex.set_option(dctenergy.DCTE_OPT_EXACT, 1)
+
+
+def test_exact_preview_maps_and_u8_layers(ex):
+    """Preview semantics in the exact mode (every pixel refined in fp64: no
+    sliding kernel for the preview window, whose regions are small): the maps
+    AND the drawn u8 layers equal the reference's golden ones exactly (the
+    fast mode's u8 layer is within +-1)."""
+    for entry in manifest()["preview"]:
+        img = load_input(entry["input"])
+        E = ex.energy_map(img, entry["N"], entry["edges"], entry["textures"],
+                          semantics=dctenergy.DCTE_PREVIEW)
+        assert np.array_equal(E, load_map(entry["output"])), entry["output"]
+        u8 = ex.energy_image_u8(img, entry["N"], entry["edges"], entry["textures"],
+                                dctenergy.DCTE_NORM_PREVIEW, entry["channels"],
+                                semantics=dctenergy.DCTE_PREVIEW)
+        assert np.array_equal(u8, load_map(entry["output_u8"])), entry["output_u8"]
+
+
+def test_exact_energy_layer_and_points(ex):
+    """The u8 energy layer (display_carver_energy) and point energies in the
+    exact mode are the reference's: the layer is normalize_lqr of the oracle
+    map, the points its values."""
+    img = load_input("natural_rgb_97x41.npy")
+    for n in (2, 4, 8, 16):
+        ref = O.energy_map(img, n, 0.3, 0.7)
+        u8 = ex.energy_image_u8(img, n, 0.3, 0.7, dctenergy.DCTE_NORM_LQR, 1)
+        assert np.array_equal(u8, O.normalize_lqr(ref)), n
+        rng = np.random.default_rng(n)
+        xy = np.stack([rng.integers(0, img.shape[1], 200), rng.integers(0, img.shape[0], 200)], 1)
+        got = ex.energy_points(img, xy.astype(np.int32), n, 0.3, 0.7)
+        assert np.array_equal(got, ref[xy[:, 1], xy[:, 0]]), n

@@ -563,6 +563,32 @@ def test_multi_device_host_path_on_one_gpu(ctx, G):
                                       many.energy_image_u8(img, n, 0.3, 0.7, mode, ch)), (n, mode)
 
 
+def test_host_buffers_sharing_pages(ctx):
+    """Frame and output packed into one allocation, so they share a page at
+    unaligned addresses (the page-locking of the host path registers exactly
+    the caller's bytes; a page-rounded registration made the runtime refuse
+    the copy into the neighbour, tools/pin_probe.cpp).  Both orders, outputs
+    above and below the 1 MiB pinning threshold: identical to separately
+    allocated buffers."""
+    h, w = 1003, 520
+    img = np.random.default_rng(7).integers(0, 256, (h, w, 3), dtype=np.uint8)
+    ref = ctx.energy_map(img, 8, 0.3, 0.7)
+    ref_u8 = ctx.energy_image_u8(img, 8, 0.3, 0.7, dctenergy.DCTE_NORM_LQR)
+    A, Bf, Bu = img.nbytes, ref.nbytes, ref_u8.nbytes
+    for out_first in (False, True):
+        big = np.zeros(100 + A + Bf + 64, np.uint8)
+        o_px, o_out = (100 + Bf, 100) if out_first else (100, 100 + A)
+        px = big[o_px:o_px + A].reshape(h, w, 3)
+        px[...] = img
+        out = big[o_out:o_out + Bf].view(np.float32).reshape(h, w)
+        assert np.array_equal(ctx.energy_map(px, 8, 0.3, 0.7, out=out), ref), out_first
+        o_u8 = 100 + A + 4 if not out_first else 100 + Bf - Bu - 4
+        u8 = big[o_u8:o_u8 + Bu].reshape(h, w)
+        assert np.array_equal(ctx.energy_image_u8(px, 8, 0.3, 0.7, dctenergy.DCTE_NORM_LQR, out=u8),
+                              ref_u8), out_first
+        assert np.array_equal(px, img)
+
+
 @pytest.mark.parametrize("n", [2, 4, 8, 16])
 def test_tile_height_does_not_change_results(n):
     """DCTE_OPT_TILE_H only re-partitions the work: any tile height gives the
