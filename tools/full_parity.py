@@ -7,7 +7,10 @@ ATOL), class flips, the largest relative error, and how many pixels are
 bit-identical.
 
     python tools/full_parity.py [--size 16384] [--size16 8192] [--threads 16]
-                                [--kind natural|lineart|dots|text|grid8] [--n 8,16]
+                                [--kind natural|lineart|dots|text|grid8] [--n 8,16] [--exact]
+
+--exact runs the context in DCTE_OPT_EXACT (the sliding fp64 maps; preview
+through the fp64 pass over every pixel), where bit_identical must equal pixels.
 
 --kind other than natural takes the tie-dense frames of tools/fix_study.py
 (binary line art, isolated dots, 4-px text blocks, 8-px grid: exact edge /
@@ -33,6 +36,8 @@ def main():
     ap.add_argument("--textures", type=float, default=0.7)
     ap.add_argument("--kind", default="natural")
     ap.add_argument("--n", default="2,4,8,16", help="block sizes, comma-separated")
+    ap.add_argument("--exact", action="store_true",
+                    help="DCTE_OPT_EXACT: the bar is every pixel bit-identical")
     a = ap.parse_args()
     import torch
     import dctenergy
@@ -43,7 +48,7 @@ def main():
     lo, hi = min(e, t) / max(e, t), max(e, t) / min(e, t)
     cases = [(dctenergy.DCTE_LQR, "liblqr", bpp) for bpp in (1, 3)] + \
             [(dctenergy.DCTE_PREVIEW, "preview", bpp) for bpp in (1, 3, 4)]
-    with dctenergy.Context(ngpus=1) as ctx:
+    with dctenergy.Context(ngpus=1, exact=a.exact) as ctx:
         def make(S, bpp):
             if a.kind == "natural":
                 return synth.natural_rows(0, S, S, bpp, seed=1, device="cuda")
@@ -96,7 +101,7 @@ def main():
                         ratio = g[off] / r[off]
                         flips += int((((ratio - lo).abs() < 1e-3 * lo) |
                                       ((ratio - hi).abs() < 1e-3 * hi)).sum())
-                print(json.dumps({"kind": a.kind, "n": n, "semantics": sname, "bpp": bpp, "frame": [S, S],
+                print(json.dumps({"kind": a.kind, "exact": a.exact, "n": n, "semantics": sname, "bpp": bpp, "frame": [S, S],
                                   "edges": e, "textures": t, "pixels": S * S,
                                   "off_tolerance": bad, "class_flips": flips,
                                   "bit_identical": same, "max_rel_err": worst,
