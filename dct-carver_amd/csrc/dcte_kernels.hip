@@ -150,7 +150,10 @@ __global__ __launch_bounds__((Geo<N, SEM>::T), MapThreads<N>::min_waves) void dc
     constexpr int DPT = Gm::template dpt<BPP>();         // raw dwords per lane per row
 
     // N <= 8: raw / lum double-buffered, so a row group needs one barrier
-    // (N = 16 keeps one buffer: its LDS combine of partial maxima adds one anyway)
+    // (N = 16 keeps one buffer and three barriers per group: double-buffered
+    // luma and partial maxima with one barrier per group measured no faster,
+    // staged (+0.1 %) or with direct loads (+2.5 %), profiles/r05/n16_pipeline_ab.jsonl --
+    // this kernel is VALU-bound, not barrier-bound)
     constexpr bool kDB = S == 1;
     constexpr int NB = kDB ? 2 : 1;
     // the direct loads (below) need no raw stage
@@ -158,10 +161,14 @@ __global__ __launch_bounds__((Geo<N, SEM>::T), MapThreads<N>::min_waves) void dc
                                 LW - kThreads > 0 && (LW - kThreads) * G <= 64;
     __shared__ uint32_t raw[kDirectLds ? 1 : NB][kDirectLds ? 1 : G][kDirectLds ? 1 : NDW];
     __shared__ float lum[NB][G][LWP];
-    // S = 4 (N = 16): per-wave partial maxima of the group's rows; only the
-    // waves owning k1 = 0 (q = 0) and k1 = 1 (q = 2) carry an edge candidate
-    __shared__ float part_t[S == 4 ? G : 1][S == 4 ? 4 : 1][S == 4 ? 64 : 1];
-    __shared__ float part_e[S == 4 ? G : 1][S == 4 ? 2 : 1][S == 4 ? 64 : 1];
+    // S = 4 (N = 16): the group's rows' maxima over the four waves, met by
+    // LDS atomic max on the bits (non-negative floats order as their bits);
+    // only the waves owning k1 = 0 (q = 0) and k1 = 1 (q = 2) carry an edge
+    // candidate.  Zero between uses (the combine resets what it read).  One
+    // slot per pixel and ds_max instead of a slot per wave and three fmax:
+    // -0.7 % per launch (profiles/r05/n16_pipeline_ab.jsonl)
+    __shared__ uint32_t part_t[S == 4 ? G : 1][S == 4 ? 64 : 1];
+    __shared__ uint32_t part_e[S == 4 ? G : 1][S == 4 ? 64 : 1];
     // refinement lists per 64-column strip (one wave's columns; N = 16: the tile)
     constexpr int SPT = S == 1 ? TW / 64 : 1;        // strips per tile
     __shared__ unsigned nflag[SPT];                  // pixels each strip flagged
@@ -334,6 +341,12 @@ __global__ __launch_bounds__((Geo<N, SEM>::T), MapThreads<N>::min_waves) void dc
     unsigned* strip_list = p.fix_list + (size_t)strip * (size_t)(64 * p.tile_h);
     const int sx0 = x0 + 64 * sc;                    // first column of the strip
     if (tx < SPT) nflag[tx] = 0;
+    if constexpr (S == 4) {
+        for (int e = tx; e < G * 64; e += kThreads) {
+            (&part_t[0][0])[e] = 0u;
+            (&part_e[0][0])[e] = 0u;
+        }
+    }
     // the next launch's dirty-strip and dense counters (stream order: nothing
     // reads them before this launch ends) -- in every launch, whatever its N
     // or semantics: the phases alternate over all launches of the stream
@@ -445,26 +458,27 @@ __global__ __launch_bounds__((Geo<N, SEM>::T), MapThreads<N>::min_waves) void dc
                     float mt, me;
                     Cols<N>::template run<(u + 1) % N>(ring, lane_p, mt, me);
                     if constexpr (S == 4) {
-                        part_t[u][lane_p][c] = mt;
-                        if ((lane_p & 1) == 0) part_e[u][lane_p >> 1][c] = me;
+                        atomicMax(&part_t[u][c], __float_as_uint(mt));
+                        if ((lane_p & 1) == 0) atomicMax(&part_e[u][c], __float_as_uint(me));
                     } else {
                         emit(ys + i - (N - 1), x, mt, me);
                     }
                 }
             }
         });
+    };
+    // N = 16: the four waves' maxima of group g (complete after a barrier
+    // that follows every wave's compute(g)); wave q finishes rows u = q mod 4
+    // and zeroes what it read
+    auto combine = [&](int g) __attribute__((always_inline)) {
         if constexpr (S == 4) {
-            // combine the four waves' maxima; wave q finishes rows u = q mod 4
-            __syncthreads();
 #pragma unroll
             for (int u = lane_p; u < G; u += 4) {
                 const int i = g * G + u;
-                if (i >= N - 1 && i < n_in) {
-                    emit(ys + i - (N - 1), x,
-                         fmaxf(fmaxf(part_t[u][0][c], part_t[u][1][c]),
-                               fmaxf(part_t[u][2][c], part_t[u][3][c])),
-                         fmaxf(part_e[u][0][c], part_e[u][1][c]));
-                }
+                if (i >= N - 1 && i < n_in)
+                    emit(ys + i - (N - 1), x, __uint_as_float(part_t[u][c]), __uint_as_float(part_e[u][c]));
+                part_t[u][c] = 0u;
+                part_e[u][c] = 0u;
             }
         }
     };
@@ -560,6 +574,10 @@ __global__ __launch_bounds__((Geo<N, SEM>::T), MapThreads<N>::min_waves) void dc
             __syncthreads();
             set_prio(false, g);
             compute(g, 0);
+            if constexpr (S == 4) {
+                __syncthreads();
+                combine(g);
+            }
         }
     }
     __syncthreads();
