@@ -2,7 +2,10 @@
 update_emap hook: served fractions and the time spent in
 the update callbacks per seam.
 
-    python tools/resize_bench.py [--size 1024x768] [--seams 16] [--n 8]
+    python tools/resize_bench.py [--size 1024x768] [--seams 16] [--n 8] [--exact]
+
+--exact sets DCTE_PLUGIN_EXACT: the maps and the hook's
+band updates in the reference's fp64 arithmetic.
 
 Uses the fake liblqr of tests/fake_lqr (energy build + per seam: DP, carve,
 update_emap over the band liblqr re-evaluates [liblqr, unverified]); the
@@ -24,13 +27,15 @@ def main():
     ap.add_argument("--seams", type=int, default=16)
     ap.add_argument("--n", type=int, default=8)
     ap.add_argument("--transposed", action="store_true")
+    ap.add_argument("--exact", action="store_true", help="DCTE_PLUGIN_EXACT")
     ap.add_argument("--verify", action="store_true",
                     help="re-run the original body on every hook-served callback (not timed fairly)")
     a = ap.parse_args()
     import numpy as np
     import torch
     from dctenergy import synth
-    from test_plugin_shim import resize
+    from test_plugin_shim import fake, resize
+    fake().fake_set_plugin_flags(2 if a.exact else 0)
     w, h = (int(v) for v in a.size.split("x"))
     img = synth.natural_rows(0, h, w, 3, seed=0, device="cuda").cpu().numpy()
     for hook in (False, True):
@@ -39,6 +44,7 @@ def main():
         upd = r["callbacks"] - r["initial"]
         print(json.dumps({
             "frame": f"{w}x{h} RGB", "n": a.n, "seams": a.seams, "transposed": a.transposed,
+            "exact": a.exact,
             "hook": hook, "callbacks": r["callbacks"], "build_callbacks": r["initial"],
             "update_callbacks": upd, "update_callbacks_per_seam": round(upd / a.seams, 1),
             "served_gpu": r["callbacks"] - r["fallback"],
