@@ -296,9 +296,9 @@ int run_exact(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, i
     DCTE_HIP(ctx, hipSetDevice(d.id));
     int tile_h = ctx->tile_h;
     if (tile_h <= 0) {
-        const int tw = dcte::exact_tile_w(n);
+        const int tw = dcte::exact_tile_w(n, sem);
         tile_h = pick_tile_h(n, rows_a, rows_b, (w + tw - 1) / tw,
-                             (long long)device_cus(d) * dcte::exact_blocks_per_cu(n, bpp),
+                             (long long)device_cus(d) * dcte::exact_blocks_per_cu(n, bpp, sem),
                              dcte::exact_default_tile_h(n));
     }
     if (tile_h > (rows_a > rows_b ? rows_a : rows_b)) tile_h = rows_a > rows_b ? rows_a : rows_b;

@@ -773,17 +773,334 @@ hipError_t launch_exact_small(const MapParams& p, hipStream_t s)
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ preview
+// The GTK preview's energies (dct_energy_preview_rows, src/render.c:31-79,
+// 421-479): the luma is RGB2LUMINANCE truncated to guchar (src/render.h:5,
+// convert_row_to_luminance :62-79) -- a small integer, as a double -- the
+// window data[dy][dx] with offsets -(c - 1) .. N - c, c = (N - 1) / 2
+// (src/dct.h:8-9, src/render.c:43-49), clamped to the region, then the same
+// dctNxN and last-maximum scan.  The window is stored the other way round
+// from liblqr's data[dx][dy], so the pass that can be shared swaps direction:
+//  * N = 8, 16 (dcte_exact_pv): ddct8x8s / ddct16x16s pass 1 runs along the
+//    FIRST index -- dy here: a vertical transform V of each window column,
+//    the same doubles for the N pixels whose windows hold that column.  A
+//    wave owns 64 consecutive columns; lane l keeps a ring of its column's
+//    last N lumas, computes V once per (column, row) and the wave swaps the V
+//    vectors through a wave-private LDS row; lanes 0 .. 64 - N then run pass
+//    2 (col8 / col16, as the liblqr kernels' pass 2) over lanes l .. l + N - 1
+//    -- dcte_exact_small's structure with the reference's 8 / 16-point steps.
+//  * N = 2, 4 (dcte_exact_pvs): ddct2d transforms along the SECOND index first
+//    -- dx here: a horizontal transform of each window row, the same doubles
+//    for the N pixels below each other: a register ring down the strip, as
+//    dcte_exact8.
+template <int BPP>
+__device__ __forceinline__ void fill_lut_pv(double* lut, int tx, int nthreads)
+{
+    if constexpr (BPP >= 3) {
+        for (int v = tx; v < 256; v += nthreads) {   // RGB2LUMINANCE's terms, left to right
+            lut[v] = 16.0 + v * 0.2568;
+            lut[256 + v] = v * 0.5041;
+            lut[512 + v] = v * 0.0979;
+        }
+    }
+}
+template <int BPP>
+__device__ __forceinline__ double luma_pv(const double* lut, uint32_t wd)
+{
+    if constexpr (BPP == 1) return (double)(wd & 255u);
+    else return (double)(unsigned char)((lut[wd & 255u] + lut[256 + ((wd >> 8) & 255u)]) + lut[512 + ((wd >> 16) & 255u)]);
+}
+
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+constexpr int kExPT = 256;                         // 4 independent waves
+
+template <int N, int BPP>
+__global__ __launch_bounds__(kExPT) void dcte_exact_pv(const MapParams p)
+{
+    constexpr int C = (N - 1) / 2, HL = C - 1, HR = N - C, G = 8, OW = 64 - (N - 1);
+    // V rows per wave: two by row parity (N = 8: no sync before the next
+    // row's writes), one for N = 16 (16 KB per wave otherwise)
+    constexpr int NV = N == 8 ? 2 : 1;
+    __shared__ double lut[BPP == 1 ? 1 : 768];
+    __shared__ double vrow[kExPT / 64][NV][N][64];
+
+    const int tx = threadIdx.x, l = tx & 63, wv = tx >> 6;
+    int bx, by;
+    xcd_tile(bx, by);
+    const int xs = (bx * (kExPT / 64) + wv) * OW;      // first output column of the wave
+    const int x = xs + l;
+    int ys, ye;
+    tile_rows(p, by, ys, ye);
+    const int n_in = (ye - ys) + N - 1;
+    const int ngroups = (n_in + G - 1) / G;
+    const int w = p.w, h = p.h;
+    const int xcol = clampx(x - HL, 0, w - 1);         // lane l's column: window column 0 of pixel x
+
+    Frame fr;
+    fr.init(p, BPP, (bx + 1) * (kExPT / 64) * OW + 64 >= w && min(h - 1, ye - 1 + HR) >= p.in_row0 + p.in_rows - 1);
+    fill_lut_pv<BPP>(lut, tx, kExPT);
+    const double we = (double)p.edges, wt = (double)p.textures;
+    __syncthreads();
+    if (xs >= w) return;                               // wave-uniform; no barrier follows
+
+    auto row_of = [&](int i) { return clampx(ys - HL + (i < n_in ? i : n_in - 1), 0, h - 1); };
+    uint2 pend[2][G];
+    auto issue = [&](int g, int b) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < G; u++) pend[b][u] = fr.fetch(fr.at(xcol, row_of(g * G + u), BPP));
+    };
+    double ring[N];                                    // luma of the column's last N input rows
+    const bool emits = l < OW && x < w;
+    float* const orow = p.out + (long long)(ys - p.y0) * p.out_stride + x;
+    const int ll = l < OW ? l : OW - 1;
+
+    // group g of parity B (static: the ring slot of row g G + u is (B G + u) mod N)
+    auto compute = [&](int g, auto B) __attribute__((always_inline)) {
+        constexpr int b = decltype(B)::value;
+        sfor<G>([&](auto U) __attribute__((always_inline)) {
+            constexpr int u = decltype(U)::value;
+            constexpr int sl = (b * G + u) % N;
+            const int i = g * G + u;
+            if (i < n_in) {
+                const uint32_t off = fr.at(xcol, row_of(i), BPP) & 3u;
+                ring[sl] = luma_pv<BPP>(lut, __builtin_amdgcn_alignbyte(pend[b][u].y, pend[b][u].x, off));
+                if (i >= N - 1) {
+                    // pass 1 along dy: window line ii = input row i - N + 1 + ii
+                    double v[N];
+#pragma unroll
+                    for (int j = 0; j < N; j++) v[j] = ring[(sl + 1 + j) % N];
+                    if constexpr (N == 8) r64::step8(v, 1);
+                    else r64::step16(v, 1);
+                    double* vr = &vrow[wv][NV == 2 ? (u & 1) : 0][0][0];
+                    if constexpr (NV == 1) wave_lds_sync();   // the previous row's reads are done
+#pragma unroll
+                    for (int k = 0; k < N; k++) vr[k * 64 + l] = v[k];
+                    wave_lds_sync();
+                    // pass 2 along dx for each k1 = a[k1][0 .. N - 1] over lanes ll ..
+                    // ll + N - 1; k1 >= 2 in a loop (one body: the kernel's code
+                    // stays in the instruction cache)
+                    double a01, m0, a10, mp = 0.0;
+                    const double* q = vr + ll;
+                    if constexpr (N == 8) {
+                        double dummy;
+                        col8<0>(q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7], a01, m0);
+                        q += 64;
+                        col8<1>(q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7], a10, mp);
+#pragma unroll 1
+                        for (int k1 = 2; k1 < 8; k1++) {
+                            q += 64;
+                            col8<2>(q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7], dummy, mp);
+                        }
+                    } else {
+                        double hv[16], acc, x0, x1, c1;
+#pragma unroll
+                        for (int j = 0; j < 16; j++) hv[j] = q[j];
+                        col16(hv, acc, x0, x1, c1);            // k1 = 0: C01 and C0,2..15 (C00 not scanned)
+                        a01 = fabs(c1);
+                        m0 = fmax(acc, fabs(K16::c8 * (x0 - x1)));
+                        q += 64;
+#pragma unroll
+                        for (int j = 0; j < 16; j++) hv[j] = q[j];
+                        col16(hv, acc, x0, x1, c1);            // k1 = 1: C10 apart
+                        a10 = fabs(K16::c8 * (x0 + x1));
+                        mp = fmax(fmax(acc, fabs(c1)), fabs(K16::c8 * (x0 - x1)));
+#pragma unroll 1
+                        for (int k1 = 2; k1 < 16; k1++) {
+                            q += 64;
+#pragma unroll
+                            for (int j = 0; j < 16; j++) hv[j] = q[j];
+                            col16(hv, acc, x0, x1, c1);
+                            mp = fmax(mp, fmax(fmax(acc, fabs(c1)), K16::c8 * (fabs(x0) + fabs(x1))));
+                        }
+                    }
+                    const double M = fmax(fmax(mp, a10), fmax(m0, a01));
+                    const bool edge = !(mp == M) && (a10 == M || (!(m0 == M) && a01 == M));
+                    if (emits) orow[(long long)(i - (N - 1)) * p.out_stride] = (float)(M * weight(edge, we, wt));
+                }
+            }
+        });
+    };
+
+    constexpr std::integral_constant<int, 0> I0{};
+    constexpr std::integral_constant<int, 1> I1{};
+    issue(0, 0);
+    for (int g = 0; g < ngroups; g += 2) {
+        if (g + 1 < ngroups) issue(g + 1, 1);
+        compute(g, I0);
+        if (g + 1 >= ngroups) break;
+        if (g + 2 < ngroups) issue(g + 2, 0);
+        compute(g + 1, I1);
+    }
+}
+
+template <int N, int BPP>
+hipError_t launch_exact_pv(const MapParams& p, hipStream_t s)
+{
+    constexpr int per_wg = (kExPT / 64) * (64 - (N - 1));
+    dim3 grid((p.w + per_wg - 1) / per_wg, p.tiles_y);
+    hipLaunchKernelGGL((dcte_exact_pv<N, BPP>), grid, dim3(kExPT), 0, s, p);
+    return hipGetLastError();
+}
+
+// N = 2, 4: lane = output column, walking down the strip (dcte_exact8's
+// structure): per input row the horizontal ddct of the lane's window row
+// (lum[b][u][tx .. tx + N - 1]) into slot `row mod N` of an N x N ring, then
+// for each k2 the vertical ddct over the ring and the scan
+template <int N, int BPP>
+__global__ __launch_bounds__(kEx8T) void dcte_exact_pvs(const MapParams p)
+{
+    constexpr int C = (N - 1) / 2, HL = C - 1, G = 8, T = kEx8T, LW = T + N - 1;
+    constexpr int HR = N - C;
+    constexpr int XH = LW - T;                        // halo columns past one per lane
+    __shared__ double lut[BPP == 1 ? 1 : 768];
+    __shared__ double lum[2][G][LW];
+
+    const int tx = threadIdx.x;
+    int bx, by;
+    xcd_tile(bx, by);
+    const int x0 = bx * T, x = x0 + tx;
+    int ys, ye;
+    tile_rows(p, by, ys, ye);
+    const int n_in = (ye - ys) + N - 1;
+    const int ngroups = (n_in + G - 1) / G;
+    const int w = p.w, h = p.h;
+
+    Frame fr;
+    fr.init(p, BPP, x0 + T + HR - 1 >= w - 1 && min(h - 1, ye - 1 + HR) >= p.in_row0 + p.in_rows - 1);
+    fill_lut_pv<BPP>(lut, tx, T);
+    const double ct[2] = {p.ct[0], 0.0};
+    const double wkr = p.ct[1] - p.ct[3], wki = p.ct[1] + p.ct[3];   // dctsub's k = 1 twiddle
+
+    auto row_of = [&](int i) { return clampx(ys - HL + (i < n_in ? i : n_in - 1), 0, h - 1); };
+    const int xc = clampx(x - HL, 0, w - 1);
+    const int hl = tx - (T - 64);                     // last wave: halo conversions
+    const bool has_halo = hl >= 0 && hl < XH * G;
+    const int hrow = has_halo ? hl / XH : 0;
+    const int hxc = clampx(x0 + T - HL + (has_halo ? hl % XH : 0), 0, w - 1);
+
+    uint2 pend[G], hpend = make_uint2(0u, 0u);
+    auto issue = [&](int g) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < G; u++) pend[u] = fr.fetch(fr.at(xc, row_of(g * G + u), BPP));
+        if (has_halo) hpend = fr.fetch(fr.at(hxc, row_of(g * G + hrow), BPP));
+    };
+    auto convert = [&](int g, int b) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < G; u++) {
+            const uint32_t off = fr.at(xc, row_of(g * G + u), BPP) & 3u;
+            lum[b][u][tx] = luma_pv<BPP>(lut, __builtin_amdgcn_alignbyte(pend[u].y, pend[u].x, off));
+        }
+        if (has_halo) {
+            const uint32_t off = fr.at(hxc, row_of(g * G + hrow), BPP) & 3u;
+            lum[b][hrow][T + hl % XH] = luma_pv<BPP>(lut, __builtin_amdgcn_alignbyte(hpend.y, hpend.x, off));
+        }
+    };
+
+    const double we = (double)p.edges, wt = (double)p.textures;
+    float* const orow = p.out + (long long)(ys - p.y0) * p.out_stride + x;
+    const bool inside = x < w;
+    double ring[N][N];                                // ring[slot][k2], slot = input row mod N
+
+    auto compute = [&](int g, int b) __attribute__((always_inline)) {
+        sfor<G>([&](auto U) __attribute__((always_inline)) {
+            constexpr int u = decltype(U)::value;
+            const int i = g * G + u;
+            if (i < n_in) {
+                // the second index first (dx): window row = input row i
+                double* r = ring[u % N];
+#pragma unroll
+                for (int k = 0; k < N; k++) r[k] = lum[b][u][tx + k];
+                ddct_small<N>(ring[u % N], ct, wkr, wki);
+                if (i >= N - 1) {
+                    // then the first (dy) for each k2: line ii = input row i - N + 1 + ii
+                    double a01 = 0.0, m0 = -1.0, a10 = 0.0, mp = 0.0;
+#pragma unroll
+                    for (int k2 = 0; k2 < N; k2++) {
+                        double hv[N];
+#pragma unroll
+                        for (int j = 0; j < N; j++) hv[j] = ring[(u + 1 + j) % N][k2];
+                        ddct_small<N>(hv, ct, wkr, wki);
+                        // C[k1][k2] = hv[k1]
+#pragma unroll
+                        for (int k1 = 0; k1 < N; k1++) {
+                            const double a = fabs(hv[k1]);
+                            if (k1 == 0 && k2 == 0) continue;              // C00 is not scanned
+                            if (k1 == 0 && k2 == 1) a01 = a;
+                            else if (k1 == 0) m0 = fmax(m0, a);
+                            else if (k1 == 1 && k2 == 0) a10 = a;
+                            else mp = fmax(mp, a);
+                        }
+                    }
+                    const double M = fmax(fmax(mp, a10), fmax(m0, a01));
+                    const bool edge = !(mp == M) && (a10 == M || (!(m0 == M) && a01 == M));
+                    if (inside) orow[(long long)(i - (N - 1)) * p.out_stride] = (float)(M * weight(edge, we, wt));
+                }
+            }
+        });
+    };
+
+    issue(0);
+    __syncthreads();                                  // lut
+    for (int g = 0; g < ngroups; g++) {
+        const int b = g & 1;
+        convert(g, b);
+        if (g + 1 < ngroups) issue(g + 1);
+        __syncthreads();
+        compute(g, b);
+    }
+}
+
+template <int N, int BPP>
+hipError_t launch_exact_pvs(const MapParams& p, hipStream_t s)
+{
+    dim3 grid((p.w + kEx8T - 1) / kEx8T, p.tiles_y);
+    hipLaunchKernelGGL((dcte_exact_pvs<N, BPP>), grid, dim3(kEx8T), 0, s, p);
+    return hipGetLastError();
+}
+
+template <int BPP>
+hipError_t launch_preview_exact(int n, const MapParams& p, hipStream_t s)
+{
+    if (n == 8) return launch_exact_pv<8, BPP>(p, s);
+    if (n == 16) return launch_exact_pv<16, BPP>(p, s);
+    if (n == 4) return launch_exact_pvs<4, BPP>(p, s);
+    if (n == 2) return launch_exact_pvs<2, BPP>(p, s);
+    return hipErrorInvalidValue;
+}
+
+template <int BPP>
+int preview_blocks_per_cu(int n)
+{
+    int v = 0;
+    hipError_t e = hipErrorInvalidValue;
+    if (n == 8) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact_pv<8, BPP>, kExPT, 0);
+    else if (n == 16) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact_pv<16, BPP>, kExPT, 0);
+    else if (n == 4) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact_pvs<4, BPP>, kEx8T, 0);
+    else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact_pvs<2, BPP>, kEx8T, 0);
+    return e == hipSuccess ? v : 0;
+}
+
 }  // namespace
 
-// workgroups of the exact kernel for (n, bpp) one CU holds at once; cached
-int exact_blocks_per_cu(int n, int bpp)
+// workgroups of the exact kernel for (n, bpp, sem) one CU holds at once; cached
+int exact_blocks_per_cu(int n, int bpp, int sem)
 {
-    static std::atomic<int> cache[4][2];
-    const int ni = n == 2 ? 0 : (n == 4 ? 1 : (n == 8 ? 2 : 3)), bi = bpp == 1 ? 0 : 1;
-    int v = cache[ni][bi].load(std::memory_order_relaxed);
+    static std::atomic<int> cache[2][4][3];
+    const int ni = n == 2 ? 0 : (n == 4 ? 1 : (n == 8 ? 2 : 3)), bi = bpp == 1 ? 0 : (bpp == 3 ? 1 : 2);
+    const int si = sem == kSemLqr ? 0 : 1;
+    int v = cache[si][ni][bi].load(std::memory_order_relaxed);
     if (v) return v;
     hipError_t e = hipErrorInvalidValue;
-    if (n == 8) e = bpp == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact8<1>, kEx8T, 0)
+    if (si == 1) {
+        v = bpp == 1 ? preview_blocks_per_cu<1>(n) : (bpp == 3 ? preview_blocks_per_cu<3>(n) : preview_blocks_per_cu<4>(n));
+        e = v > 0 ? hipSuccess : hipErrorInvalidValue;
+    } else if (n == 8) e = bpp == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact8<1>, kEx8T, 0)
                                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact8<3>, kEx8T, 0);
     else if (n == 16) e = bpp == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact16<1>, kEx16T, 0)
                                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact16<3>, kEx16T, 0);
@@ -792,13 +1109,17 @@ int exact_blocks_per_cu(int n, int bpp)
     else e = bpp == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact_small<2, 1>, kExST, 0)
                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact_small<2, 3>, kExST, 0);
     if (e != hipSuccess || v <= 0) v = 1;
-    cache[ni][bi].store(v, std::memory_order_relaxed);
+    cache[si][ni][bi].store(v, std::memory_order_relaxed);
     return v;
 }
 
-bool exact_supported(int n, int sem) { return sem == kSemLqr && (n == 2 || n == 4 || n == 8 || n == 16); }
-int exact_tile_w(int n)
+bool exact_supported(int n, int sem)
 {
+    return (sem == kSemLqr || sem == kSemPreview) && (n == 2 || n == 4 || n == 8 || n == 16);
+}
+int exact_tile_w(int n, int sem)
+{
+    if (sem != kSemLqr) return (n == 8 || n == 16) ? (kExPT / 64) * (64 - (n - 1)) : kEx8T;
     return n == 8 ? kEx8T : (n == 16 ? 64 : (kExST / 64) * (64 - (n - 1)));
 }
 int exact_default_tile_h(int n) { return DCTE_EX_TILE_H; }
@@ -806,6 +1127,12 @@ int exact_default_tile_h(int n) { return DCTE_EX_TILE_H; }
 hipError_t launch_map_exact(int n, int bpp, int sem, const MapParams& p, hipStream_t s)
 {
     if (p.tiles_y <= 0) return hipSuccess;
+    if (sem == kSemPreview) {
+        if (bpp == 1) return launch_preview_exact<1>(n, p, s);
+        if (bpp == 3) return launch_preview_exact<3>(n, p, s);
+        if (bpp == 4) return launch_preview_exact<4>(n, p, s);
+        return hipErrorInvalidValue;
+    }
     if (sem != kSemLqr) return hipErrorInvalidValue;
     if (n == 8) {
         if (bpp == 1) return launch_exact8<1>(p, s);

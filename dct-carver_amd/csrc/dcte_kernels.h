@@ -194,9 +194,9 @@ int dense_batch_entries(int n, int sem);   // entries per dense refinement batch
 // the exact map (dcte_exact.hip, DCTE_OPT_EXACT): the reference's fp64
 // arithmetic in a sliding window, no refinement launch
 hipError_t launch_map_exact(int n, int bpp, int sem, const MapParams& p, hipStream_t s);
-bool exact_supported(int n, int sem);   // else the exact mode refines every pixel of the fp32 map
-int exact_tile_w(int n);                // output columns per workgroup
+bool exact_supported(int n, int sem);   // (every N, both semantics since r05)
+int exact_tile_w(int n, int sem);       // output columns per workgroup
 int exact_default_tile_h(int n);
-int exact_blocks_per_cu(int n, int bpp);
+int exact_blocks_per_cu(int n, int bpp, int sem);
 
 }  // namespace dcte

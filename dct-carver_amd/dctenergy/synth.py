@@ -10,7 +10,10 @@ import math
 
 def _hash_uniform(idx, seed, torch):
     # splitmix64-style finaliser on int64 (wrapping arithmetic), -> (0, 1)
-    z = idx * 0x5851F42D4C957F2D + (seed * 0x14057B7EF767814F + 0x2545F4914F6CDD1D)
+    # the seed's term wrapped to int64 here (torch takes ints below 2^64 and
+    # wraps them the same way, so seeds that fit give the frames they always gave)
+    k = (seed * 0x14057B7EF767814F + 0x2545F4914F6CDD1D) & 0xFFFFFFFFFFFFFFFF
+    z = idx * 0x5851F42D4C957F2D + (k - (1 << 64) if k >= (1 << 63) else k)
     z = z ^ ((z >> 31) & 0x1FFFFFFFF)
     z = z * 0x7FB5D329728EA185
     z = z ^ ((z >> 27) & 0x1FFFFFFFFF)

@@ -240,10 +240,9 @@ def test_exact_off_again_is_the_fast_map(ex):
 
 
 def test_exact_preview_maps_and_u8_layers(ex):
-    """Preview semantics in the exact mode (every pixel refined in fp64: no
-    sliding kernel for the preview window, whose regions are small): the maps
-    AND the drawn u8 layers equal the reference's golden ones exactly (the
-    fast mode's u8 layer is within +-1)."""
+    """Preview semantics in the exact mode (dcte_exact_pv / dcte_exact_pvs):
+    the maps AND the drawn u8 layers equal the reference's golden ones
+    exactly (the fast mode's u8 layer is within +-1)."""
     for entry in manifest()["preview"]:
         img = load_input(entry["input"])
         E = ex.energy_map(img, entry["N"], entry["edges"], entry["textures"],
@@ -268,3 +267,95 @@ def test_exact_energy_layer_and_points(ex):
         xy = np.stack([rng.integers(0, img.shape[1], 200), rng.integers(0, img.shape[0], 200)], 1)
         got = ex.energy_points(img, xy.astype(np.int32), n, 0.3, 0.7)
         assert np.array_equal(got, ref[xy[:, 1], xy[:, 0]]), n
+
+
+PV = dctenergy.DCTE_PREVIEW
+
+
+@pytest.mark.parametrize("n", [2, 4, 8, 16])
+def test_exact_preview_shapes_and_borders(ex, n):
+    """The preview window (offsets -(c - 1) .. N - c, data[dy][dx], u8 luma)
+    through the preview's sliding kernels: ragged shapes from 1 x 1 up, grey,
+    RGB and RGBA, both weightings -- every pixel bit-identical."""
+    shapes = [(1, 1), (1, 300), (300, 1), (2, 3), (5, 7), (8, 8), (17, 255), (33, 256),
+              (9, 257), (130, 129), (129, 513), (260, 700)]
+    for shape in shapes:
+        rng = np.random.default_rng(hash((n, 7) + shape) & 0xFFFF)
+        for bpp in (1, 3, 4):
+            img = rng.integers(0, 256, shape + ((bpp,) if bpp > 1 else ()), dtype=np.uint8)
+            for e, t in ((0.15, 0.85), (0.5, 0.5)):
+                ref = O.preview_map(img, n, e, t, nthreads=NTHREADS)
+                got = ex.energy_map(img, n, e, t, semantics=PV)
+                assert np.array_equal(got, ref), (shape, bpp, e, t)
+
+
+def test_exact_preview_tile_heights_and_strides(ex):
+    img = load_input("natural_rgb_97x41.npy")
+    pad = np.zeros((41, 110, 3), np.uint8)
+    pad[:, :97] = img
+    ref = {n: O.preview_map(img, n, 0.3, 0.7) for n in (2, 4, 8, 16)}
+    for n in (2, 4, 8, 16):
+        assert np.array_equal(ex.energy_map(pad[:, :97], n, 0.3, 0.7, semantics=PV), ref[n]), n
+    try:
+        for th in (1, 2, 7, 8, 9, 33, 64):
+            ex.set_option(dctenergy.DCTE_OPT_TILE_H, th)
+            for n in (2, 4, 8, 16):
+                assert np.array_equal(ex.energy_map(img, n, 0.3, 0.7, semantics=PV), ref[n]), (th, n)
+    finally:
+        ex.set_option(dctenergy.DCTE_OPT_TILE_H, 0)
+
+
+@pytest.mark.parametrize("n", [2, 4, 8, 16])
+def test_exact_preview_tie_dense_frames(ex, n):
+    torch = _torch()
+    S = 1024
+    rng = np.random.default_rng(50 + n)
+    for name, img in _tie_frames(S, rng).items():
+        got = torch.from_numpy(ex.energy_map(img, n, 0.3, 0.7, semantics=PV)).cuda()
+        _equal_dev(got, O.preview_map(img, n, 0.3, 0.7, nthreads=NTHREADS), f"preview {name} {S}^2 N={n}")
+
+
+def test_exact_preview_bands(ex):
+    """Preview row bands (the preview's own halo: c - 1 rows above, N - c
+    below) and a two-range launch == the full preview map."""
+    torch = _torch()
+    from dctenergy import synth
+    H, W = 300, 517
+    frame = synth.natural_rows(0, H, W, 4, seed=4, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    for n in (2, 4, 8, 16):
+        full = torch.empty((H, W), dtype=torch.float32, device="cuda")
+        ex.energy_map_tensor(frame, full, n, 0.3, 0.7, semantics=PV)
+        torch.cuda.synchronize()
+        assert np.array_equal(full.cpu().numpy(), O.preview_map(frame.cpu().numpy(), n, 0.3, 0.7,
+                                                                 nthreads=NTHREADS)), n
+        c = (n - 1) // 2
+        up, down = max(0, c - 1), max(0, n - c)
+        parts = torch.full((H, W), -1.0, dtype=torch.float32, device="cuda")
+        cuts = [0, 1, 2, 130, 131, 299, 300]
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            lo, hi = max(0, a - up), min(H - 1, b - 1 + down)
+            band = frame[lo:hi + 1].clone()
+            ex.energy_map_tensor(band, parts[a:b], n, 0.3, 0.7, h=H, in_row0=lo, y0=a, y1=b, semantics=PV)
+        torch.cuda.synchronize()
+        assert torch.equal(full, parts), n
+        got = torch.full((H, W), -1.0, dtype=torch.float32, device="cuda")
+        ex.energy_map_device2(frame.data_ptr(), frame.stride(0), W, H, 4, 0, H, 0, 3, 296, 300, n,
+                              0.3, 0.7, got.data_ptr(), got.stride(0), st, semantics=PV)
+        torch.cuda.synchronize()
+        want = torch.full((H, W), -1.0, dtype=torch.float32, device="cuda")
+        want[0:3] = full[0:3]
+        want[296:300] = full[296:300]
+        assert torch.equal(got, want), n
+
+
+@pytest.mark.parametrize("n,S", [(8, 4096), (16, 4096), (4, 4096), (2, 4096)])
+def test_exact_preview_full_frames(ex, n, S):
+    torch = _torch()
+    from dctenergy import synth
+    frame = synth.natural_rows(0, S, S, 3, seed=n, device="cuda")
+    out = torch.empty((S, S), dtype=torch.float32, device="cuda")
+    ex.energy_map_tensor(frame, out, n, 0.3, 0.7, semantics=PV)
+    torch.cuda.synchronize()
+    ref = O.preview_map(frame.cpu().numpy(), n, 0.3, 0.7, nthreads=NTHREADS)
+    _equal_dev(out, ref, f"preview {S}^2 RGB N={n}")
