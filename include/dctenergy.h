@@ -108,10 +108,9 @@ extern "C" {
                                own fp64 operation order (ddct8x8s / ddct16x16s /
                                ddct2d and the last-maximum scan) by a sliding-
                                window kernel, so liblqr's DP on it carves the
-                               reference's seams.  Where no such kernel exists
-                                every pixel of the fp32 map is
-                               refined in fp64 instead -- the same bits, slower.
-                               Seam-band updates and point energies are then
+                               reference's seams -- every N, both semantics
+                               (the preview's transposed window has kernels of
+                               its own).  Seam-band updates and point energies are then
                                refined in fp64 too.  0 = the fp32 map with the
                                tie refinement (default; <= 1e-5 relative). */
 
