@@ -153,8 +153,8 @@ int bad_arg(dcte_ctx* ctx, const char* what)
 bool valid_n(int n) { return n == 2 || n == 4 || n == 8 || n == 16; }
 
 // the refinement margin a call uses: the exact mode refines every pixel it
-// does not compute in fp64 outright (seam bands, points, and the block sizes /
-// semantics dcte_exact.hip has no sliding kernel for)
+// does not compute in fp64 outright (seam bands and points; every map call
+// goes to dcte_exact.hip's sliding kernels)
 double eff_tau(const dcte_ctx* ctx) { return ctx->exact ? 1.0 : ctx->tie_tau; }
 
 // window offsets -hl .. +hr of a semantics
