@@ -320,6 +320,9 @@ __global__ __launch_bounds__(kEx8T, DCTE_EX_MINW) void dcte_exact8(const MapPara
         });
     };
 
+    // (loads issued just before their conversion instead -- nothing in
+    // flight across the passes: 178 VGPRs, no faster at 2 waves, and at the
+    // 3-wave cap (spilling) +3.5 %, profiles/r05/exact_occupancy_ab.jsonl)
     issue(0);
     __syncthreads();                                  // lut
     for (int g = 0; g < ngroups; g++) {
@@ -929,6 +932,9 @@ __global__ __launch_bounds__(kExPT) void dcte_exact_pv(const MapParams p)
 
     constexpr std::integral_constant<int, 0> I0{};
     constexpr std::integral_constant<int, 1> I1{};
+    // (issuing a group's loads only as it starts saves 10-12 VGPRs but ran
+    // +0.4 % / +1.1 %, and +1 % / +4 % at a 4-wave cap:
+    // profiles/r05/exact_occupancy_ab.jsonl)
     issue(0, 0);
     for (int g = 0; g < ngroups; g += 2) {
         if (g + 1 < ngroups) issue(g + 1, 1);
