@@ -221,42 +221,52 @@ DCTE_HD void dct16_odd_rows(const float d[8], int k0, float out[4])
 //   v_n = d_{2n} + i d_{7-2n},  u_n = v_n exp(-i pi (4n+1)/32)      (pre-twiddle)
 //   U_k = sum_n u_n exp(-2 pi i n k / 4)                            (DFT-4)
 //   Y_{2k} = Re W_k, Y_{7-2k} = -Im W_k,  W_k = U_k exp(-i pi k / 8)  (post-twiddle)
-// with the post-twiddle in scaled form: k = 0 is free (scale sqrt2, chain m2);
-// k = 1 and k = 3 are sqrt2 cos(pi/8) = E times one FMA per output (chain mE:
-// tan(pi/8) for k = 1, cot(3 pi/8) = tan(pi/8) for k = 3); k = 2 gives
-// max(|Ur + Ui|, |Ur - Ui|) = |Ur| + |Ui| at scale sqrt2 cos(pi/4) = 1
-// (chain m).  37 VALU ops instead of the 48 of the DCT-IV-via-DCT-II
-// recursion (X[2m+1] = E[m] - X[2m-1] over an 8-point transform of the
-// pre-scaled d, which r02 used).
-constexpr float k16c0 = 0.99518472667219693f;   // cos( 1 pi/32)
-constexpr float k16s0 = 0.098017140329560604f;  // sin( 1 pi/32)
-constexpr float k16c1 = 0.88192126434835505f;   // cos( 5 pi/32)
-constexpr float k16s1 = 0.47139673682599764f;   // sin( 5 pi/32)
-constexpr float k16c2 = 0.63439328416364549f;   // cos( 9 pi/32)
-constexpr float k16s2 = 0.77301045336273699f;   // sin( 9 pi/32)
-constexpr float k16c3 = 0.29028467725446233f;   // cos(13 pi/32)
-constexpr float k16s3 = 0.95694033573220894f;   // sin(13 pi/32)
-constexpr float k16s2c = 1.4142135623730951f;   // sqrt2 (scale of the m2 chain)
+// all in scaled form (r05): each pre-twiddle is one FMA per output with its
+// larger factor sigma_n = max(cos, sin) pulled out (ratio t_n <= 1), and the
+// DFT's additions absorb the ratios of those factors (sigma_2 / sigma_0,
+// sigma_3 / sigma_1, sigma_1 / sigma_0) as one FMA each, so every U_k comes
+// out at the common scale sigma_0 = cos(pi/32).  The post-twiddle as before:
+// k = 0 free (chain m2, scale sqrt2 sigma_0); k = 1 and 3 one FMA per output
+// with tan(pi/8) (chain mE, scale E sigma_0); k = 2 max(|Ur + Ui|, |Ur - Ui|)
+// = |Ur| + |Ui| (chain m, scale sigma_0).  The chains are the odd half's own
+// (their scales differ from the even half's by sigma_0): 33 VALU ops, r04's
+// form (two per pre-twiddle output) took 41.
+constexpr float k16t0 = 0.09849140335716425f;   // tan( 1 pi/32)         (sigma_0 = cos)
+constexpr float k16t1 = 0.5345111359507916f;    // tan( 5 pi/32)         (sigma_1 = cos)
+constexpr float k16t2 = 0.8206787908286602f;    // cot( 9 pi/32)         (sigma_2 = sin)
+constexpr float k16t3 = 0.30334668360734235f;   // cot(13 pi/32)         (sigma_3 = sin)
+constexpr float k16r02 = 0.7767507203889779f;   // sigma_2 / sigma_0
+constexpr float k16r13 = 1.085063230037077f;    // sigma_3 / sigma_1
+constexpr float k16r01 = 0.8861885042161126f;   // sigma_1 / sigma_0
+constexpr float k16s2c = 1.4142135623730951f;   // sqrt2
+constexpr float k16oM = 0.9951847266721969f;    // sigma_0: scale of the odd m chain
+constexpr float k16oE = 1.300271507080512f;     // E sigma_0: the odd mE chain
+constexpr float k16o2 = 1.4074037375263826f;    // sqrt2 sigma_0: the m2 chain (and the C01 edge)
 
 template <bool EDGE = false>
 DCTE_HD void dct16_odd_sc(const float d[8], float& m, float& mE, float& m2, float* edge = nullptr)
 {
-    // u_n = (a + i b)(cos - i sin) = (a cos + b sin) + i (b cos - a sin)
-    float r0 = fmaf(d[7], k16s0, d[0] * k16c0), i0 = fmaf(d[0], -k16s0, d[7] * k16c0);
-    float r1 = fmaf(d[5], k16s1, d[2] * k16c1), i1 = fmaf(d[2], -k16s1, d[5] * k16c1);
-    float r2 = fmaf(d[3], k16s2, d[4] * k16c2), i2 = fmaf(d[4], -k16s2, d[3] * k16c2);
-    float r3 = fmaf(d[1], k16s3, d[6] * k16c3), i3 = fmaf(d[6], -k16s3, d[1] * k16c3);
-    float sr = r0 + r2, si = i0 + i2, tr = r1 + r3, ti = i1 + i3;
-    float dr = r0 - r2, di = i0 - i2, er = r1 - r3, ei = i1 - i3;
+    // u_n / sigma_n: (a + t b) + i (b - t a) for sigma = cos, (t a + b) + i (t b - a) for sigma = sin
+    const float R0 = fmaf(d[7], k16t0, d[0]), I0 = fmaf(d[0], -k16t0, d[7]);
+    const float R1 = fmaf(d[5], k16t1, d[2]), I1 = fmaf(d[2], -k16t1, d[5]);
+    const float R2 = fmaf(d[4], k16t2, d[3]), I2 = fmaf(d[3], k16t2, -d[4]);
+    const float R3 = fmaf(d[6], k16t3, d[1]), I3 = fmaf(d[1], k16t3, -d[6]);
+    // DFT-4 at scale sigma_0 (s = u0 + u2, dd = u0 - u2 at sigma_0; t = u1 + u3, e = u1 - u3 at sigma_1)
+    const float sr = fmaf(R2, k16r02, R0), si = fmaf(I2, k16r02, I0);
+    const float dr = fmaf(R2, -k16r02, R0), di = fmaf(I2, -k16r02, I0);
+    const float tr = fmaf(R3, k16r13, R1), ti = fmaf(I3, k16r13, I1);
+    const float er = fmaf(R3, -k16r13, R1), ei = fmaf(I3, -k16r13, I1);
     // U0 = (s + t), U2 = (s - t), U1 = (dr + ei) + i (di - er), U3 = (dr - ei) + i (di + er)
+    const float u0r = fmaf(tr, k16r01, sr), u0i = fmaf(ti, k16r01, si);
     if constexpr (EDGE) {                       // X1 = sqrt2 Re U0 is the edge atom C01
-        *edge = fabsf(sr + tr);
-        m2 = fmaxf(m2, fabsf(si + ti));
+        *edge = fabsf(u0r);
+        m2 = fmaxf(m2, fabsf(u0i));
     } else {
-        m2 = max2in(m2, sr + tr, si + ti);
+        m2 = max2in(m2, u0r, u0i);
     }
-    m = fmaxf(m, fabsf(sr - tr) + fabsf(si - ti));
-    float u1r = dr + ei, u1i = di - er, u3r = dr - ei, u3i = di + er;
+    m = fmaxf(m, fabsf(fmaf(tr, -k16r01, sr)) + fabsf(fmaf(ti, -k16r01, si)));
+    const float u1r = fmaf(ei, k16r01, dr), u1i = fmaf(er, -k16r01, di);
+    const float u3r = fmaf(ei, -k16r01, dr), u3i = fmaf(er, k16r01, di);
     mE = max2in(mE, fmaf(u1i, k8rEF, u1r), fmaf(u1r, k8rEF, -u1i));
     mE = max2in(mE, fmaf(u3r, k8rEF, u3i), fmaf(u3i, -k8rEF, u3r));
 }
@@ -264,9 +274,9 @@ DCTE_HD void dct16_odd_sc(const float d[8], float& m, float& mE, float& m2, floa
 // An all-texture column of the N = 16 second pass: the even half (the 8-point transform of s, same hat
 // units) in the scaled form of dct8_col_sc and the odd half through
 // dct16_odd_sc: magnitudes go to the running maxima m (scale 1), mE, mA, mQ
-// and m2.
+// (even half) and mO, mEO, m2 (odd half, scales k16oM, k16oE, k16o2).
 DCTE_HD void dct16_tex_sc(const float x[16], float& m, float& mE, float& mA, float& mQ,
-                          float& m2)
+                          float& mO, float& mEO, float& m2)
 {
     float s[8], d[8];
 #pragma unroll
@@ -280,7 +290,7 @@ DCTE_HD void dct16_tex_sc(const float x[16], float& m, float& mE, float& mA, flo
     mA = max2in(mA, ya[0], ya[1]);
     mQ = fmaxf(mQ, pq);
     m = fmaxf(m, v1);
-    dct16_odd_sc<false>(d, m, mE, m2);
+    dct16_odd_sc<false>(d, mO, mEO, m2);
 }
 
 }  // namespace dcte

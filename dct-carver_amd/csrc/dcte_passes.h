@@ -145,6 +145,7 @@ struct Cols<16> {
         mt = 0.0f;
         me = 0.0f;
         float mE = 0.0f, mA = 0.0f, mQ = 0.0f, m2 = 0.0f;   // scaled running maxima (dct16_tex_sc)
+        float mO = 0.0f, mEO = 0.0f;                         // ... of the odd halves
         // channel 0: k1 = 4q' ... special roles for k1 = 0 (q = 0) and k1 = 1 (q = 2)
 #pragma unroll
         for (int j = 0; j < 16; j++) col[j] = ring[(O + j) & 15][0];
@@ -172,22 +173,22 @@ struct Cols<16> {
             mA = max2in(mA, ya[0], ya[1]);
             mQ = pq;
             if (q == 0) {
-                dct16_odd_sc<true>(d, mt, mE, m2, &e_odd);
-                me = e_odd * k16s2c;
+                dct16_odd_sc<true>(d, mO, mEO, m2, &e_odd);
+                me = e_odd * k16o2;
             } else {
-                dct16_odd_sc<false>(d, mt, mE, m2);
+                dct16_odd_sc<false>(d, mO, mEO, m2);
                 me = e_even;
             }
         } else {
-            dct16_tex_sc(col, mt, mE, mA, mQ, m2);
+            dct16_tex_sc(col, mt, mE, mA, mQ, mO, mEO, m2);
         }
 #pragma unroll
         for (int c = 1; c < 4; c++) {
 #pragma unroll
             for (int j = 0; j < 16; j++) col[j] = ring[(O + j) & 15][c];
-            dct16_tex_sc(col, mt, mE, mA, mQ, m2);
+            dct16_tex_sc(col, mt, mE, mA, mQ, mO, mEO, m2);
         }
-        mt = max2in(max2in(mt, mQ * k8sPQ, mE * k8sE), mA * k8sA, m2 * k16s2c);
+        mt = max2in(max2in(max2in(mt, mQ * k8sPQ, mE * k8sE), mA * k8sA, m2 * k16o2), mO * k16oM, mEO * k16oE);
     }
 };
 

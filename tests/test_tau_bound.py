@@ -8,8 +8,10 @@ integer pixel windows (random restarts of six window kinds) for the largest
     delta = max(|m_e32 - m_e|, |m_t32 - m_t|) / max(m_e, m_t)
 with the map kernel's own fp32 code against the exact transform, and this
 test demands delta <= tau/4 (2x margin on top of the tau/2 requirement).
-The long searches (10-20 M windows per case) are in
-profiles/r02/tau_search.jsonl; the worst found there is 5.6e-7 = tau/7.
+The long searches (1.5-20 M windows per case, tools/tau_long.py) are in
+profiles/r05/tau_search.jsonl (re-run in r05 after the N = 16 odd half
+moved to a scaled form; N = 2, 4, 8 reproduce r02's exactly); the worst
+found there is 5.5e-7 = tau/7.
 Reference arithmetic: src/fft2d/shrtdct.c:61-117, 238-386,
 src/fft2d/fftsg2d.c:566-627, decision src/dct.c:100-109.
 """
@@ -45,7 +47,7 @@ def test_committed_long_search_margin():
     import json
     import os
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                        "profiles", "r02", "tau_search.jsonl")
+                        "profiles", "r05", "tau_search.jsonl")
     rows = [json.loads(l) for l in open(path)]
     assert {r["n"] for r in rows} == {2, 4, 8, 16}
     for r in rows:
