@@ -157,7 +157,11 @@ __global__ __launch_bounds__((Geo<N, SEM>::T), MapThreads<N>::min_waves) void dc
     constexpr bool kDB = S == 1;
     constexpr int NB = kDB ? 2 : 1;
     // the direct loads (below) need no raw stage
-    constexpr bool kDirectLds = S == 1 && kDB && !(N <= DCTE_PF2_MAXN) &&
+    // raw rows two groups ahead (N <= 4; N = 4 colour layers take the direct
+    // loads below instead: 16384^2 RGB 0.534 -> 0.486 ms; grey and N = 2 are
+    // faster two groups ahead, profiles/r05/small_n_direct_ab.jsonl)
+    constexpr bool kPF2 = S == 1 && N <= DCTE_PF2_MAXN && !(N == 4 && BPP >= 3);
+    constexpr bool kDirectLds = S == 1 && kDB && !kPF2 &&
                                 LW - kThreads > 0 && (LW - kThreads) * G <= 64;
     __shared__ uint32_t raw[kDirectLds ? 1 : NB][kDirectLds ? 1 : G][kDirectLds ? 1 : NDW];
     __shared__ float lum[NB][G][LWP];
@@ -230,7 +234,7 @@ __global__ __launch_bounds__((Geo<N, SEM>::T), MapThreads<N>::min_waves) void dc
 
     // raw rows in flight: PFD groups ahead (two register buffers for the
     // small blocks, whose launches are bound by loads in flight, not VALU)
-    constexpr int PFD = (S == 1 && N <= DCTE_PF2_MAXN) ? 2 : 1;
+    constexpr int PFD = kPF2 ? 2 : 1;
     uint32_t pref[PFD][G][DPT];
     auto issue = [&](int g, auto PB) {
 #pragma unroll
