@@ -359,3 +359,24 @@ def test_exact_preview_full_frames(ex, n, S):
     torch.cuda.synchronize()
     ref = O.preview_map(frame.cpu().numpy(), n, 0.3, 0.7, nthreads=NTHREADS)
     _equal_dev(out, ref, f"preview {S}^2 RGB N={n}")
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_exact_multi_device_host_path(G):
+    """The single-process multi-device host path (band split, halo rows, the
+    per-device chunk pipelines, transposed strips) in the exact mode: every
+    pixel the reference's, for both semantics."""
+    if dctenergy.device_count() == 0:
+        pytest.skip("no device")
+    rng = np.random.default_rng(G)
+    img = rng.integers(0, 256, (2100, 301, 3), dtype=np.uint8)
+    img[:, 100:200] //= 7
+    with dctenergy.Context(ngpus=G, same_device=True, exact=True) as many:
+        for n in (2, 8, 16):
+            assert np.array_equal(many.energy_map(img, n, 0.3, 0.7),
+                                  O.energy_map(img, n, 0.3, 0.7, nthreads=NTHREADS)), n
+            assert np.array_equal(many.energy_map(img[:700], n, 0.3, 0.7, transposed=True),
+                                  O.energy_map(np.ascontiguousarray(np.swapaxes(img[:700], 0, 1)), n, 0.3, 0.7,
+                                               nthreads=NTHREADS)), n
+            assert np.array_equal(many.energy_map(img, n, 0.3, 0.7, semantics=PV),
+                                  O.preview_map(img, n, 0.3, 0.7, nthreads=NTHREADS)), n
