@@ -53,6 +53,8 @@ def parse(argv=None):
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--no-stress", action="store_true",
                     help="skip the tie-dense (line-art) frame timed after the headline")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the configs[1] / configs[4] timings after the headline")
     ap.add_argument("--no-exact", action="store_true",
                     help="skip the DCTE_OPT_EXACT (bit-identical fp64) map timed after the headline")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -293,6 +295,52 @@ def stress(ctx, n, S, e, t, dev, stream, iters=10, rounds=3):
 # from the kernels (DESIGN.md §3 "exact map"); the N = 16 figure includes the
 # pass-1 work the eight waves of a column repeat (246 instead of 114 per pixel)
 EXACT_FP64_OPS = {2: 21, 4: 105, 8: 425, 16: 2270}
+def other_configs(ctx, e, t, dev, stream, iters=20, rounds=3):
+    """BASELINE configs[1] (4096^2 RGB, N = 8) and configs[4] (8192^2 RGB,
+    N = 16) on this GPU, timed like the headline after it, on the same kind of
+    synthetic natural-like frame: call_ms = map + refinement per call (HIP
+    events on the stream; the headline's step), map_ms = the map launches
+    alone (HIP events around each); best of `rounds` rounds of `iters`."""
+    import torch
+    import dctenergy
+    from dctenergy import synth
+    res = {}
+    st = torch.cuda.current_stream(dev)
+    for S, n, key in ((4096, 8, "config2_4096_rgb_n8"), (8192, 16, "config5_8192_rgb_n16")):
+        fr = synth.natural_rows(0, S, S, 3, seed=0, device=dev)
+        out = torch.empty((S, S), dtype=torch.float32, device=dev)
+
+        def call():
+            ctx.energy_map_device(fr.data_ptr(), fr.stride(0), S, S, 3, 0, S, 0, S, n, e, t,
+                                  out.data_ptr(), out.stride(0), stream)
+        for _ in range(3):
+            call()
+        torch.cuda.synchronize()
+        best_call, best_map = 1e9, 1e9
+        for _ in range(rounds):
+            ctx.profile_read()
+            ctx.set_option(dctenergy.DCTE_OPT_PROFILE, 1)
+            a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a0.record(st)
+            for _ in range(iters):
+                call()
+            a1.record(st)
+            torch.cuda.synchronize()
+            ctx.set_option(dctenergy.DCTE_OPT_PROFILE, 0)
+            launches, kms = ctx.profile_read()
+            best_call = min(best_call, a0.elapsed_time(a1) / iters)
+            best_map = min(best_map, kms / max(1, launches))
+        res[key] = {"frame": f"{S}x{S} RGB natural-like, N={n}, e={e}, t={t}",
+                    "call_ms": round(best_call, 4), "map_ms": round(best_map, 4),
+                    "value": round(S * S / best_call / 1e3, 1), "unit": "Mpx/s",
+                    "hbm_frac_of_map": round(S * S * 7 / (best_map * 1e-3) / 8.0e12, 4)}
+        del fr, out
+    torch.cuda.empty_cache()
+    res["what"] = ("BASELINE configs[1] and configs[4] after the timed region (the headline is "
+                   "configs[2]); call = map + tie refinement, as the headline's step")
+    return res
+
+
 # gfx950 fp64 VALU: 16 lanes / clk / SIMD x 1024 SIMDs x 2.4 GHz
 FP64_PEAK_OPS = 256 * 4 * 16 * 2.4e9
 
@@ -713,6 +761,8 @@ def main():
             res["stress"] = stress(ctx, n, S, e, t, dev, stream)
         if world == 1 and not args.no_exact:
             res["exact"] = exact(n, S, e, t, dev, buf)
+        if world == 1 and not args.no_configs and S == 16384 and n == 8:
+            res["configs_1gpu"] = other_configs(ctx, e, t, dev, stream)
         if world == 1 and not args.no_host_path:
             res["host_path"] = host_path(ctx, buf, n, e, t)
             if S > 4096:                       # BASELINE configs[1]'s frame size, a 4096^2 crop
