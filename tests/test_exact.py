@@ -9,7 +9,9 @@ not a tolerance.  Covered: every golden map, borders and odd shapes, strided
 rows, row bands and two-range launches, BASELINE configs 2, 3 and 5 over every
 pixel, tie-dense frames (line art, dots, an 8-px grid: exact edge/texture ties
 decided only by the reference's rounding), and the carve loop (liblqr's DP on
-the exact map cuts the reference's seams).
+the exact map cuts the reference's seams); the preview semantics through
+their own kernels (golden maps and u8 layers, shapes, strides, tile heights,
+bands, tie-dense and 4096^2 frames); the multi-device host path.
 """
 import os
 
