@@ -779,3 +779,25 @@ def test_injected_launch_failure_then_good_call(ctx, which, n):
             ctx.energy_map_tensor(frame, after, n, 0.3, 0.7)
             torch.cuda.synchronize()
             assert torch.equal(after, before), (which, profile)
+
+
+@pytest.mark.parametrize("shape", [(33, 65537), (65537, 19), (3, 100003)])
+def test_extreme_aspect_ratios(ctx, shape):
+    """Frames past 65 536 columns (or rows) and only a few rows (or columns)
+    tall: more column tiles than any square config, tile heights far above
+    the frame, the border clamp on both sides of every window -- every N,
+    both semantics, grey and RGB: within tolerance of the oracle, and the
+    exact mode bit-identical."""
+    rng = np.random.default_rng(shape[1])
+    NT = max(1, min(16, len(os.sched_getaffinity(0))))
+    for bpp in (1, 3):
+        img = rng.integers(0, 256, shape + ((bpp,) if bpp > 1 else ()), dtype=np.uint8)
+        img[:, ::7] //= 5                               # some smooth stretches: ties, refinement
+        with dctenergy.Context(ngpus=1, exact=True) as ex:
+            for n in (2, 4, 8, 16):
+                ref = O.energy_map(img, n, 0.3, 0.7, nthreads=NT)
+                assert within_tol(ctx.energy_map(img, n, 0.3, 0.7), ref).all(), (shape, bpp, n)
+                assert np.array_equal(ex.energy_map(img, n, 0.3, 0.7), ref), (shape, bpp, n)
+                pv = O.preview_map(img, n, 0.3, 0.7, nthreads=NT)
+                assert within_tol(ctx.energy_map(img, n, 0.3, 0.7, semantics=dctenergy.DCTE_PREVIEW), pv).all()
+                assert np.array_equal(ex.energy_map(img, n, 0.3, 0.7, semantics=dctenergy.DCTE_PREVIEW), pv)
