@@ -801,3 +801,23 @@ def test_extreme_aspect_ratios(ctx, shape):
                 pv = O.preview_map(img, n, 0.3, 0.7, nthreads=NT)
                 assert within_tol(ctx.energy_map(img, n, 0.3, 0.7, semantics=dctenergy.DCTE_PREVIEW), pv).all()
                 assert np.array_equal(ex.energy_map(img, n, 0.3, 0.7, semantics=dctenergy.DCTE_PREVIEW), pv)
+
+
+def test_frames_past_one_buffer_resource_are_refused(ctx):
+    """A launch addresses its readable rows through one 32-bit buffer
+    resource: a row span of 4 GiB or more is refused with DCTE_ERANGE before
+    anything is read (here a huge rowstride over a small buffer), in both
+    modes, and the context stays usable."""
+    torch = _torch()
+    small = torch.zeros((4, 64, 3), dtype=torch.uint8, device="cuda")
+    out = torch.empty((4, 64), dtype=torch.float32, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    with dctenergy.Context(ngpus=1, exact=True) as ex:
+        for c in (ctx, ex):
+            with pytest.raises(dctenergy.DcteError) as e:
+                c.energy_map_device(small.data_ptr(), 1 << 31, 64, 4, 3, 0, 4, 0, 4, 8, 0.3, 0.7,
+                                    out.data_ptr(), out.stride(0), st)
+            assert e.value.code == dctenergy.DCTE_ERANGE
+            c.energy_map_tensor(small, out, 8, 0.3, 0.7)
+            torch.cuda.synchronize()
+            assert torch.equal(out, torch.zeros_like(out))
