@@ -10,8 +10,10 @@ with the map kernel's own fp32 code against the exact transform, and this
 test demands delta <= tau/4 (2x margin on top of the tau/2 requirement).
 The long searches (1.5-20 M windows per case, tools/tau_long.py) are in
 profiles/r05/tau_search.jsonl (re-run in r05 after the N = 16 odd half
-moved to a scaled form; N = 2, 4, 8 reproduce r02's exactly); the worst
-found there is 5.5e-7 = tau/7.
+moved to a scaled form; N = 2, 4, 8 reproduce r02's exactly) and, 7.5x
+longer for N = 16, in profiles/r05/tau_search_n16_long.jsonl; the worst found
+is 7.7e-7 = tau/5.2 (N = 16 grey; r04's N = 16 arithmetic at the same budget:
+7.5e-7, tau_search_n16_long_r04arith.jsonl).
 Reference arithmetic: src/fft2d/shrtdct.c:61-117, 238-386,
 src/fft2d/fftsg2d.c:566-627, decision src/dct.c:100-109.
 """
@@ -46,9 +48,10 @@ def test_committed_long_search_margin():
     """The committed long searches all stay within tau/4."""
     import json
     import os
-    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                        "profiles", "r05", "tau_search.jsonl")
-    rows = [json.loads(l) for l in open(path)]
+    base = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "r05")
+    rows = [json.loads(l) for l in open(os.path.join(base, "tau_search.jsonl"))]
+    # plus r05's 7.5x longer N = 16 searches (15 M windows per case, six seeds)
+    rows += [json.loads(l) for l in open(os.path.join(base, "tau_search_n16_long.jsonl"))]
     assert {r["n"] for r in rows} == {2, 4, 8, 16}
     for r in rows:
         assert r["delta"] <= EM.TIE_TAU / 4, r
