@@ -299,8 +299,9 @@ int run_exact(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, i
         const int tw = dcte::exact_tile_w(n, sem);
         tile_h = pick_tile_h(n, rows_a, rows_b, (w + tw - 1) / tw,
                              (long long)device_cus(d) * dcte::exact_blocks_per_cu(n, bpp, sem),
-                             dcte::exact_default_tile_h(n));
+                             dcte::exact_default_tile_h(n, sem));
     }
+    if (tile_h > dcte::exact_max_tile_h(n, sem)) tile_h = dcte::exact_max_tile_h(n, sem);
     if (tile_h > (rows_a > rows_b ? rows_a : rows_b)) tile_h = rows_a > rows_b ? rows_a : rows_b;
     const int tiles_a = (rows_a + tile_h - 1) / tile_h;
     const int tiles_y = tiles_a + (rows_b + tile_h - 1) / tile_h;

@@ -784,7 +784,8 @@ hipError_t launch_exact_small(const MapParams& p, hipStream_t s)
 // (src/dct.h:8-9, src/render.c:43-49), clamped to the region, then the same
 // dctNxN and last-maximum scan.  The window is stored the other way round
 // from liblqr's data[dx][dy], so the pass that can be shared swaps direction:
-//  * N = 8, 16 (dcte_exact_pv): ddct8x8s / ddct16x16s pass 1 runs along the
+//  * N = 16 (dcte_exact_pv; N = 8 since r05 through dcte_exact_pv8t below,
+//    dcte_exact8 on its side): ddct8x8s / ddct16x16s pass 1 runs along the
 //    FIRST index -- dy here: a vertical transform V of each window column,
 //    the same doubles for the N pixels whose windows hold that column.  A
 //    wave owns 64 consecutive columns; lane l keeps a ring of its column's
@@ -954,6 +955,142 @@ hipError_t launch_exact_pv(const MapParams& p, hipStream_t s)
     return hipGetLastError();
 }
 
+// N = 8, transposed (dcte_exact_pv8t, r05): dcte_exact8 turned on its side.
+// A lane owns one output ROW of a 256-row tile and walks RIGHT along a
+// 128-column strip; per input column it runs pass 1 (along dy: the column's
+// 8 window lumas, staged in LDS as lumT[column][row]) into slot `column mod
+// 8` of a 64-double register ring and, for every complete window, the 8
+// pass-2 steps over the ring (col8, along dx) and the decision.  Every lane
+// emits (no halo lanes), nothing crosses lanes, and pass 1 runs once per
+// (row, column) as in dcte_exact8.
+// (16384^2 RGB 4.22 -> 3.75 ms against dcte_exact_pv<8>, grey 4.07 -> 3.59:
+// profiles/r05/exact_preview8_transposed_ab.jsonl; dcte_exact_pv now serves N = 16)
+constexpr int kExPTT = 256;                        // lanes = output rows per tile
+constexpr int kExPTW = 128;                        // output columns per workgroup
+
+template <int BPP>
+__global__ __launch_bounds__(kExPTT, DCTE_EX_MINW) void dcte_exact_pv8t(const MapParams p)
+{
+    constexpr int N = 8, C = (N - 1) / 2, HL = C - 1, HR = N - C, G = 8, T = kExPTT, TW = kExPTW;
+    constexpr int LR = T + N - 1;                      // luma rows staged per column
+    // input column i = global column x0 - HL - 1 + i (one column before the
+    // first window, so that group g >= 1 completes the windows of output
+    // columns x0 + 8 (g - 1) .. + 7: a lane stores them as two aligned float4)
+    constexpr int NC = TW + N;
+    constexpr int CONV = (G * LR + T - 1) / T;         // conversions per thread and group
+    __shared__ double lut[BPP == 1 ? 1 : 768];
+    __shared__ double lumT[2][G][LR];                  // [buffer][column of the group][row]
+
+    const int tx = threadIdx.x;
+    int bx, by;
+    xcd_tile(bx, by);
+    const int x0 = bx * TW;
+    int ys, ye;
+    tile_rows(p, by, ys, ye);
+    const int w = p.w, h = p.h;
+    const int ngroups = (NC + G - 1) / G;
+
+    Frame fr;
+    fr.init(p, BPP, x0 + TW + HR - 1 >= w - 1 && min(h - 1, ys + LR - 1 - HL) >= p.in_row0 + p.in_rows - 1);
+    fill_lut_pv<BPP>(lut, tx, T);
+
+    // conversion k of a group: element e = tx + T k -> row e / G, column e % G
+    // (a wave's loads cover 8 neighbouring columns of 8 rows)
+    auto col_of = [&](int g, int c) { return clampx(x0 - HL - 1 + g * G + c, 0, w - 1); };
+    auto row_of = [&](int r) { return clampx(ys - HL + r, 0, h - 1); };
+    uint2 pend[CONV];
+    auto issue = [&](int g) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < CONV; k++) {
+            const int e = tx + T * k;
+            if (CONV * T == G * LR || e < G * LR) pend[k] = fr.fetch(fr.at(col_of(g, e % G), row_of(e / G), BPP));
+        }
+    };
+    auto convert = [&](int g, int b) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < CONV; k++) {
+            const int e = tx + T * k;
+            if (CONV * T == G * LR || e < G * LR) {
+                const uint32_t off = fr.at(col_of(g, e % G), row_of(e / G), BPP) & 3u;
+                lumT[b][e % G][e / G] = luma_pv<BPP>(lut, __builtin_amdgcn_alignbyte(pend[k].y, pend[k].x, off));
+            }
+        }
+    };
+
+    const double we = (double)p.edges, wt = (double)p.textures;
+    const int y = ys + tx;
+    const bool row_ok = y < ye;
+    float* const orow = p.out + (long long)((row_ok ? y : ys) - p.y0) * p.out_stride;
+    double ring[N][N];                                // ring[slot][k1], slot = input column mod 8
+    float res[G];                                     // the group's outputs (columns x0 + 8 (g - 1) + u)
+
+    auto compute = [&](int g, int b) __attribute__((always_inline)) {
+        sfor<G>([&](auto U) __attribute__((always_inline)) {
+            constexpr int u = decltype(U)::value;          // input column g G + u
+            static_assert(NC % G == 0, "whole groups");
+            {
+                // pass 1 along dy (the first index): window line of the column,
+                // rows y - HL .. y + HR = staged rows tx .. tx + 7
+                double* r = ring[u];
+#pragma unroll
+                for (int k = 0; k < N; k++) r[k] = lumT[b][u][tx + k];
+                r64::step8(r, 1);
+                if (g > 0) {
+                    // pass 2 along dx over the ring: window column j = input column i - 7 + j
+                    constexpr int s0 = (u + 1) % 8, s1 = (u + 2) % 8, s2 = (u + 3) % 8, s3 = (u + 4) % 8;
+                    constexpr int s4 = (u + 5) % 8, s5 = (u + 6) % 8, s6 = (u + 7) % 8, s7 = u;
+                    double a01, m0, a10, mp = 0.0;
+#define DCTE_COL(ROLE, K, A, M) \
+    col8<ROLE>(ring[s0][K], ring[s1][K], ring[s2][K], ring[s3][K], ring[s4][K], ring[s5][K], ring[s6][K], ring[s7][K], A, M)
+                    DCTE_COL(0, 0, a01, m0);
+                    DCTE_COL(1, 1, a10, mp);
+                    double dummy;
+                    DCTE_COL(2, 2, dummy, mp);
+                    DCTE_COL(2, 3, dummy, mp);
+                    DCTE_COL(2, 4, dummy, mp);
+                    DCTE_COL(2, 5, dummy, mp);
+                    DCTE_COL(2, 6, dummy, mp);
+                    DCTE_COL(2, 7, dummy, mp);
+#undef DCTE_COL
+                    const double M = fmax(fmax(mp, a10), fmax(m0, a01));
+                    const bool edge = !(mp == M) && (a10 == M || (!(m0 == M) && a01 == M));
+                    res[u] = (float)(M * weight(edge, we, wt));
+                }
+            }
+        });
+        if (g > 0 && row_ok) {
+            const int xa = x0 + G * (g - 1);
+            float* o = orow + xa;
+            if (xa + G <= w && (reinterpret_cast<uintptr_t>(o) & 15u) == 0) {
+                reinterpret_cast<float4*>(o)[0] = make_float4(res[0], res[1], res[2], res[3]);
+                reinterpret_cast<float4*>(o)[1] = make_float4(res[4], res[5], res[6], res[7]);
+            } else {
+#pragma unroll
+                for (int u = 0; u < G; u++)
+                    if (xa + u < w) o[u] = res[u];
+            }
+        }
+    };
+
+    issue(0);
+    __syncthreads();                                  // lut
+    for (int g = 0; g < ngroups; g++) {
+        const int b = g & 1;
+        convert(g, b);
+        if (g + 1 < ngroups) issue(g + 1);
+        __syncthreads();
+        compute(g, b);
+    }
+}
+
+template <int BPP>
+hipError_t launch_exact_pv8t(const MapParams& p, hipStream_t s)
+{
+    dim3 grid((p.w + kExPTW - 1) / kExPTW, p.tiles_y);
+    hipLaunchKernelGGL((dcte_exact_pv8t<BPP>), grid, dim3(kExPTT), 0, s, p);
+    return hipGetLastError();
+}
+
 // N = 2, 4: lane = output column, walking down the strip (dcte_exact8's
 // structure): per input row the horizontal ddct of the lane's window row
 // (lum[b][u][tx .. tx + N - 1]) into slot `row mod N` of an N x N ring, then
@@ -1073,7 +1210,7 @@ hipError_t launch_exact_pvs(const MapParams& p, hipStream_t s)
 template <int BPP>
 hipError_t launch_preview_exact(int n, const MapParams& p, hipStream_t s)
 {
-    if (n == 8) return launch_exact_pv<8, BPP>(p, s);
+    if (n == 8) return launch_exact_pv8t<BPP>(p, s);
     if (n == 16) return launch_exact_pv<16, BPP>(p, s);
     if (n == 4) return launch_exact_pvs<4, BPP>(p, s);
     if (n == 2) return launch_exact_pvs<2, BPP>(p, s);
@@ -1085,7 +1222,7 @@ int preview_blocks_per_cu(int n)
 {
     int v = 0;
     hipError_t e = hipErrorInvalidValue;
-    if (n == 8) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact_pv<8, BPP>, kExPT, 0);
+    if (n == 8) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact_pv8t<BPP>, kExPTT, 0);
     else if (n == 16) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact_pv<16, BPP>, kExPT, 0);
     else if (n == 4) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact_pvs<4, BPP>, kEx8T, 0);
     else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact_pvs<2, BPP>, kEx8T, 0);
@@ -1125,10 +1262,18 @@ bool exact_supported(int n, int sem)
 }
 int exact_tile_w(int n, int sem)
 {
-    if (sem != kSemLqr) return (n == 8 || n == 16) ? (kExPT / 64) * (64 - (n - 1)) : kEx8T;
+    if (sem != kSemLqr && n == 8) return kExPTW;
+    if (sem != kSemLqr) return n == 16 ? (kExPT / 64) * (64 - (n - 1)) : kEx8T;
     return n == 8 ? kEx8T : (n == 16 ? 64 : (kExST / 64) * (64 - (n - 1)));
 }
-int exact_default_tile_h(int n) { return DCTE_EX_TILE_H; }
+int exact_default_tile_h(int n, int sem)
+{
+    return (sem != kSemLqr && n == 8) ? kExPTT : DCTE_EX_TILE_H;
+}
+int exact_max_tile_h(int n, int sem)
+{
+    return (sem != kSemLqr && n == 8) ? kExPTT : (1 << 30);   // a lane per output row
+}
 
 hipError_t launch_map_exact(int n, int bpp, int sem, const MapParams& p, hipStream_t s)
 {

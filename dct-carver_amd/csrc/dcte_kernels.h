@@ -196,7 +196,8 @@ int dense_batch_entries(int n, int sem);   // entries per dense refinement batch
 hipError_t launch_map_exact(int n, int bpp, int sem, const MapParams& p, hipStream_t s);
 bool exact_supported(int n, int sem);   // (every N, both semantics since r05)
 int exact_tile_w(int n, int sem);       // output columns per workgroup
-int exact_default_tile_h(int n);
+int exact_default_tile_h(int n, int sem);
+int exact_max_tile_h(int n, int sem);     // rows one workgroup can take (preview N = 8: its lanes)
 int exact_blocks_per_cu(int n, int bpp, int sem);
 
 }  // namespace dcte
