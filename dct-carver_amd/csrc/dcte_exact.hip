@@ -783,20 +783,19 @@ hipError_t launch_exact_small(const MapParams& p, hipStream_t s)
 // window data[dy][dx] with offsets -(c - 1) .. N - c, c = (N - 1) / 2
 // (src/dct.h:8-9, src/render.c:43-49), clamped to the region, then the same
 // dctNxN and last-maximum scan.  The window is stored the other way round
-// from liblqr's data[dx][dy], so the pass that can be shared swaps direction:
-//  * N = 16 (dcte_exact_pv; N = 8 since r05 through dcte_exact_pv8t below,
-//    dcte_exact8 on its side): ddct8x8s / ddct16x16s pass 1 runs along the
-//    FIRST index -- dy here: a vertical transform V of each window column,
-//    the same doubles for the N pixels whose windows hold that column.  A
-//    wave owns 64 consecutive columns; lane l keeps a ring of its column's
-//    last N lumas, computes V once per (column, row) and the wave swaps the V
-//    vectors through a wave-private LDS row; lanes 0 .. 64 - N then run pass
-//    2 (col8 / col16, as the liblqr kernels' pass 2) over lanes l .. l + N - 1
-//    -- dcte_exact_small's structure with the reference's 8 / 16-point steps.
-//  * N = 2, 4 (dcte_exact_pvs): ddct2d transforms along the SECOND index first
-//    -- dx here: a horizontal transform of each window row, the same doubles
-//    for the N pixels below each other: a register ring down the strip, as
-//    dcte_exact8.
+// from liblqr's data[dx][dy], so the shareable pass swaps direction and the
+// kernels turn the liblqr ones on their side:
+//  * N = 8, 16 (dcte_exact_pv8t, dcte_exact_pv16t): ddct8x8s / ddct16x16s
+//    pass 1 runs along the FIRST index -- dy here -- so a lane owns an output
+//    ROW and walks RIGHT with dcte_exact8's / dcte_exact16's register ring
+//    (one pass-1 transform per (row, column)).  r05's first preview kernels
+//    shared V across lanes through LDS as dcte_exact_small does (4.22 ms at
+//    16384^2 N = 8, 5.79 ms at 8192^2 N = 16, against 3.75 / 4.90 now:
+//    profiles/r05/exact_preview8_transposed_ab.jsonl, exact_preview16_transposed_ab.jsonl).
+//  * N = 2, 4 (dcte_exact_pvs): ddct2d transforms along the SECOND index
+//    first -- dx here: a horizontal transform of each window row, the same
+//    doubles for the N pixels below each other: a register ring down the
+//    strip, as dcte_exact8.
 template <int BPP>
 __device__ __forceinline__ void fill_lut_pv(double* lut, int tx, int nthreads)
 {
@@ -815,146 +814,6 @@ __device__ __forceinline__ double luma_pv(const double* lut, uint32_t wd)
     else return (double)(unsigned char)((lut[wd & 255u] + lut[256 + ((wd >> 8) & 255u)]) + lut[512 + ((wd >> 16) & 255u)]);
 }
 
-__device__ __forceinline__ void wave_lds_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-constexpr int kExPT = 256;                         // 4 independent waves
-
-template <int N, int BPP>
-__global__ __launch_bounds__(kExPT) void dcte_exact_pv(const MapParams p)
-{
-    constexpr int C = (N - 1) / 2, HL = C - 1, HR = N - C, G = 8, OW = 64 - (N - 1);
-    // V rows per wave: two by row parity (N = 8: no sync before the next
-    // row's writes), one for N = 16 (16 KB per wave otherwise)
-    constexpr int NV = N == 8 ? 2 : 1;
-    __shared__ double lut[BPP == 1 ? 1 : 768];
-    __shared__ double vrow[kExPT / 64][NV][N][64];
-
-    const int tx = threadIdx.x, l = tx & 63, wv = tx >> 6;
-    int bx, by;
-    xcd_tile(bx, by);
-    const int xs = (bx * (kExPT / 64) + wv) * OW;      // first output column of the wave
-    const int x = xs + l;
-    int ys, ye;
-    tile_rows(p, by, ys, ye);
-    const int n_in = (ye - ys) + N - 1;
-    const int ngroups = (n_in + G - 1) / G;
-    const int w = p.w, h = p.h;
-    const int xcol = clampx(x - HL, 0, w - 1);         // lane l's column: window column 0 of pixel x
-
-    Frame fr;
-    fr.init(p, BPP, (bx + 1) * (kExPT / 64) * OW + 64 >= w && min(h - 1, ye - 1 + HR) >= p.in_row0 + p.in_rows - 1);
-    fill_lut_pv<BPP>(lut, tx, kExPT);
-    const double we = (double)p.edges, wt = (double)p.textures;
-    __syncthreads();
-    if (xs >= w) return;                               // wave-uniform; no barrier follows
-
-    auto row_of = [&](int i) { return clampx(ys - HL + (i < n_in ? i : n_in - 1), 0, h - 1); };
-    uint2 pend[2][G];
-    auto issue = [&](int g, int b) __attribute__((always_inline)) {
-#pragma unroll
-        for (int u = 0; u < G; u++) pend[b][u] = fr.fetch(fr.at(xcol, row_of(g * G + u), BPP));
-    };
-    double ring[N];                                    // luma of the column's last N input rows
-    const bool emits = l < OW && x < w;
-    float* const orow = p.out + (long long)(ys - p.y0) * p.out_stride + x;
-    const int ll = l < OW ? l : OW - 1;
-
-    // group g of parity B (static: the ring slot of row g G + u is (B G + u) mod N)
-    auto compute = [&](int g, auto B) __attribute__((always_inline)) {
-        constexpr int b = decltype(B)::value;
-        sfor<G>([&](auto U) __attribute__((always_inline)) {
-            constexpr int u = decltype(U)::value;
-            constexpr int sl = (b * G + u) % N;
-            const int i = g * G + u;
-            if (i < n_in) {
-                const uint32_t off = fr.at(xcol, row_of(i), BPP) & 3u;
-                ring[sl] = luma_pv<BPP>(lut, __builtin_amdgcn_alignbyte(pend[b][u].y, pend[b][u].x, off));
-                if (i >= N - 1) {
-                    // pass 1 along dy: window line ii = input row i - N + 1 + ii
-                    double v[N];
-#pragma unroll
-                    for (int j = 0; j < N; j++) v[j] = ring[(sl + 1 + j) % N];
-                    if constexpr (N == 8) r64::step8(v, 1);
-                    else r64::step16(v, 1);
-                    double* vr = &vrow[wv][NV == 2 ? (u & 1) : 0][0][0];
-                    if constexpr (NV == 1) wave_lds_sync();   // the previous row's reads are done
-#pragma unroll
-                    for (int k = 0; k < N; k++) vr[k * 64 + l] = v[k];
-                    wave_lds_sync();
-                    // pass 2 along dx for each k1 = a[k1][0 .. N - 1] over lanes ll ..
-                    // ll + N - 1; k1 >= 2 in a loop (one body: the kernel's code
-                    // stays in the instruction cache)
-                    double a01, m0, a10, mp = 0.0;
-                    const double* q = vr + ll;
-                    if constexpr (N == 8) {
-                        double dummy;
-                        col8<0>(q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7], a01, m0);
-                        q += 64;
-                        col8<1>(q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7], a10, mp);
-#pragma unroll 1
-                        for (int k1 = 2; k1 < 8; k1++) {
-                            q += 64;
-                            col8<2>(q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7], dummy, mp);
-                        }
-                    } else {
-                        double hv[16], acc, x0, x1, c1;
-#pragma unroll
-                        for (int j = 0; j < 16; j++) hv[j] = q[j];
-                        col16(hv, acc, x0, x1, c1);            // k1 = 0: C01 and C0,2..15 (C00 not scanned)
-                        a01 = fabs(c1);
-                        m0 = fmax(acc, fabs(K16::c8 * (x0 - x1)));
-                        q += 64;
-#pragma unroll
-                        for (int j = 0; j < 16; j++) hv[j] = q[j];
-                        col16(hv, acc, x0, x1, c1);            // k1 = 1: C10 apart
-                        a10 = fabs(K16::c8 * (x0 + x1));
-                        mp = fmax(fmax(acc, fabs(c1)), fabs(K16::c8 * (x0 - x1)));
-#pragma unroll 1
-                        for (int k1 = 2; k1 < 16; k1++) {
-                            q += 64;
-#pragma unroll
-                            for (int j = 0; j < 16; j++) hv[j] = q[j];
-                            col16(hv, acc, x0, x1, c1);
-                            mp = fmax(mp, fmax(fmax(acc, fabs(c1)), K16::c8 * (fabs(x0) + fabs(x1))));
-                        }
-                    }
-                    const double M = fmax(fmax(mp, a10), fmax(m0, a01));
-                    const bool edge = !(mp == M) && (a10 == M || (!(m0 == M) && a01 == M));
-                    if (emits) orow[(long long)(i - (N - 1)) * p.out_stride] = (float)(M * weight(edge, we, wt));
-                }
-            }
-        });
-    };
-
-    constexpr std::integral_constant<int, 0> I0{};
-    constexpr std::integral_constant<int, 1> I1{};
-    // (issuing a group's loads only as it starts saves 10-12 VGPRs but ran
-    // +0.4 % / +1.1 %, and +1 % / +4 % at a 4-wave cap:
-    // profiles/r05/exact_occupancy_ab.jsonl)
-    issue(0, 0);
-    for (int g = 0; g < ngroups; g += 2) {
-        if (g + 1 < ngroups) issue(g + 1, 1);
-        compute(g, I0);
-        if (g + 1 >= ngroups) break;
-        if (g + 2 < ngroups) issue(g + 2, 0);
-        compute(g + 1, I1);
-    }
-}
-
-template <int N, int BPP>
-hipError_t launch_exact_pv(const MapParams& p, hipStream_t s)
-{
-    constexpr int per_wg = (kExPT / 64) * (64 - (N - 1));
-    dim3 grid((p.w + per_wg - 1) / per_wg, p.tiles_y);
-    hipLaunchKernelGGL((dcte_exact_pv<N, BPP>), grid, dim3(kExPT), 0, s, p);
-    return hipGetLastError();
-}
-
 // N = 8, transposed (dcte_exact_pv8t, r05): dcte_exact8 turned on its side.
 // A lane owns one output ROW of a 256-row tile and walks RIGHT along a
 // 128-column strip; per input column it runs pass 1 (along dy: the column's
@@ -963,8 +822,8 @@ hipError_t launch_exact_pv(const MapParams& p, hipStream_t s)
 // pass-2 steps over the ring (col8, along dx) and the decision.  Every lane
 // emits (no halo lanes), nothing crosses lanes, and pass 1 runs once per
 // (row, column) as in dcte_exact8.
-// (16384^2 RGB 4.22 -> 3.75 ms against dcte_exact_pv<8>, grey 4.07 -> 3.59:
-// profiles/r05/exact_preview8_transposed_ab.jsonl; dcte_exact_pv now serves N = 16)
+// (16384^2 RGB 4.22 -> 3.75 ms against r05's first, lane-shared preview
+// kernel, grey 4.07 -> 3.59: profiles/r05/exact_preview8_transposed_ab.jsonl)
 constexpr int kExPTT = 256;                        // lanes = output rows per tile
 constexpr int kExPTW = 128;                        // output columns per workgroup
 
@@ -1091,6 +950,145 @@ hipError_t launch_exact_pv8t(const MapParams& p, hipStream_t s)
     return hipGetLastError();
 }
 
+// N = 16, transposed (dcte_exact_pv16t, r05): dcte_exact16 on its side, as
+// dcte_exact_pv8t is dcte_exact8 on its side.  A workgroup of 8 waves owns 64
+// output ROWS (lane = row) and walks right along a strip in groups of 16
+// input columns; wave q keeps the two channels (k1 = the vertical frequency
+// here) of dcte_exact16's pairing in a 16-column ring, runs the part of pass
+// 1 (along dy) its pair needs on the column's 16 staged lumas, and pass 2
+// (along dx) over its ring; the eight partial maxima meet in LDS as in
+// dcte_exact16, and after the group's barrier all 512 threads decide the
+// group's 64 rows x 16 columns and write them row by row.
+constexpr int kExP16TW = 128;                      // output columns per workgroup
+
+template <int BPP>
+__global__ __launch_bounds__(kEx16T, DCTE_EX16_MINW) void dcte_exact_pv16t(const MapParams p)
+{
+    constexpr int N = 16, C = (N - 1) / 2, HL = C - 1, HR = N - C, G = 16, T = kEx16T, TW = kExP16TW;
+    constexpr int LR = 64 + N - 1;                     // luma rows staged per column
+    constexpr int NC = TW + N;                         // input columns (one before the first window)
+    static_assert(NC % G == 0, "whole groups");
+    constexpr int CONV = (G * LR + T - 1) / T;         // conversions per thread and group
+    __shared__ double lut[BPP == 1 ? 1 : 768];
+    __shared__ double lumT[G][LR];                     // [column of the group][row]
+    __shared__ unsigned long long pmax[G][64];         // max |C| after (1,0), as bits (atomic max)
+    __shared__ double pe[G][3][64];                    // |C01|, max |C0,2..15|, |C10|
+
+    const int tx = threadIdx.x, c = tx & 63;
+    const int q = __builtin_amdgcn_readfirstlane(tx >> 6);   // wave = channel pair
+    int bx, by;
+    xcd_tile(bx, by);
+    const int x0 = bx * TW;
+    int ys, ye;
+    tile_rows(p, by, ys, ye);
+    const int w = p.w, h = p.h;
+    constexpr int ngroups = NC / G;
+
+    Frame fr;
+    fr.init(p, BPP, x0 + TW + HR - 1 >= w - 1 && min(h - 1, ys + LR - 1 - HL) >= p.in_row0 + p.in_rows - 1);
+    fill_lut_pv<BPP>(lut, tx, T);
+    for (int e = tx; e < G * 64; e += T) pmax[e / 64][e % 64] = 0ull;
+
+    // conversion k of a group: element e = tx + T k -> row e / G, column e % G
+    auto col_of = [&](int g, int cc) { return clampx(x0 - HL - 1 + g * G + cc, 0, w - 1); };
+    auto row_of = [&](int r) { return clampx(ys - HL + r, 0, h - 1); };
+    uint2 pend[CONV];
+    auto issue = [&](int g) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < CONV; k++) {
+            const int e = tx + T * k;
+            if (CONV * T == G * LR || e < G * LR) pend[k] = fr.fetch(fr.at(col_of(g, e % G), row_of(e / G), BPP));
+        }
+    };
+    auto convert = [&](int g) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < CONV; k++) {
+            const int e = tx + T * k;
+            if (CONV * T == G * LR || e < G * LR) {
+                const uint32_t off = fr.at(col_of(g, e % G), row_of(e / G), BPP) & 3u;
+                lumT[e % G][e / G] = luma_pv<BPP>(lut, __builtin_amdgcn_alignbyte(pend[k].y, pend[k].x, off));
+            }
+        }
+    };
+
+    const double we = (double)p.edges, wt = (double)p.textures;
+    double ring[N][2];                                 // ring[slot][channel], slot = input column mod 16
+
+    auto compute = [&](int g) __attribute__((always_inline)) {
+        sfor<G>([&](auto U) __attribute__((always_inline)) {
+            constexpr int u = decltype(U)::value;
+            // pass 1 along dy (the first index): the column's window line, rows c .. c + 15
+            double v[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) v[k] = lumT[u][c + k];
+            row16_pair(q, v, ring[u][0], ring[u][1]);
+            if (g > 0) {
+                // pass 2 along dx: window column j = input column g G + u - 15 + j = slot (u + 1 + j) % 16
+                double va[16], vb[16];
+#pragma unroll
+                for (int j = 0; j < 16; j++) {
+                    va[j] = ring[(u + 1 + j) % 16][0];
+                    vb[j] = ring[(u + 1 + j) % 16][1];
+                }
+                double accb, b0, b1, bc1;
+                col16(vb, accb, b0, b1, bc1);          // channel B: never an edge atom's row
+                double mp = fmax(fmax(accb, fabs(bc1)), K16::c8 * (fabs(b0) + fabs(b1)));
+                double acca, a0, a1, ac1;
+                col16(va, acca, a0, a1, ac1);
+                if (q == 0) {                          // k1 = 0: C01 and C0,2..15 (C00 not scanned)
+                    pe[u][0][c] = fabs(ac1);
+                    pe[u][1][c] = fmax(acca, fabs(K16::c8 * (a0 - a1)));
+                } else if (q == 4) {                   // k1 = 1: C10 apart
+                    pe[u][2][c] = fabs(K16::c8 * (a0 + a1));
+                    mp = fmax(mp, fmax(fmax(acca, fabs(ac1)), fabs(K16::c8 * (a0 - a1))));
+                } else {
+                    mp = fmax(mp, fmax(fmax(acca, fabs(ac1)), K16::c8 * (fabs(a0) + fabs(a1))));
+                }
+                atomicMax(&pmax[u][c], (unsigned long long)__double_as_longlong(mp));
+            }
+        });
+    };
+    // the group's 64 rows x 16 columns, row by row: thread t -> row t / 8,
+    // columns 2 (t % 8) and 2 (t % 8) + 1 (a wave writes 8 rows x 64 bytes)
+    auto finalize = [&](int g) __attribute__((always_inline)) {
+        const int r = tx >> 3, y = ys + r, xa = x0 + G * (g - 1) + 2 * (tx & 7);
+        float o[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const int u = 2 * (tx & 7) + k;
+            const double mp = __longlong_as_double((long long)pmax[u][r]);
+            const double a01 = pe[u][0][r], m0 = pe[u][1][r], a10 = pe[u][2][r];
+            const double M = fmax(fmax(mp, a10), fmax(m0, a01));
+            const bool edge = !(mp == M) && (a10 == M || (!(m0 == M) && a01 == M));
+            o[k] = (float)(M * weight(edge, we, wt));
+            pmax[u][r] = 0ull;
+        }
+        if (y < ye) {
+            float* const dst = p.out + (long long)(y - p.y0) * p.out_stride + xa;
+            if (xa < w) dst[0] = o[0];
+            if (xa + 1 < w) dst[1] = o[1];
+        }
+    };
+
+    issue(0);
+    for (int g = 0; g < ngroups; g++) {
+        convert(g);
+        if (g + 1 < ngroups) issue(g + 1);
+        __syncthreads();             // lumT of g; the previous group's decisions done
+        compute(g);
+        __syncthreads();             // partials of g; every read of lumT done
+        if (g > 0) finalize(g);
+    }
+}
+
+template <int BPP>
+hipError_t launch_exact_pv16t(const MapParams& p, hipStream_t s)
+{
+    dim3 grid((p.w + kExP16TW - 1) / kExP16TW, p.tiles_y);
+    hipLaunchKernelGGL((dcte_exact_pv16t<BPP>), grid, dim3(kEx16T), 0, s, p);
+    return hipGetLastError();
+}
+
 // N = 2, 4: lane = output column, walking down the strip (dcte_exact8's
 // structure): per input row the horizontal ddct of the lane's window row
 // (lum[b][u][tx .. tx + N - 1]) into slot `row mod N` of an N x N ring, then
@@ -1211,7 +1209,7 @@ template <int BPP>
 hipError_t launch_preview_exact(int n, const MapParams& p, hipStream_t s)
 {
     if (n == 8) return launch_exact_pv8t<BPP>(p, s);
-    if (n == 16) return launch_exact_pv<16, BPP>(p, s);
+    if (n == 16) return launch_exact_pv16t<BPP>(p, s);
     if (n == 4) return launch_exact_pvs<4, BPP>(p, s);
     if (n == 2) return launch_exact_pvs<2, BPP>(p, s);
     return hipErrorInvalidValue;
@@ -1223,7 +1221,7 @@ int preview_blocks_per_cu(int n)
     int v = 0;
     hipError_t e = hipErrorInvalidValue;
     if (n == 8) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact_pv8t<BPP>, kExPTT, 0);
-    else if (n == 16) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact_pv<16, BPP>, kExPT, 0);
+    else if (n == 16) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact_pv16t<BPP>, kEx16T, 0);
     else if (n == 4) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact_pvs<4, BPP>, kEx8T, 0);
     else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, dcte_exact_pvs<2, BPP>, kEx8T, 0);
     return e == hipSuccess ? v : 0;
@@ -1262,17 +1260,18 @@ bool exact_supported(int n, int sem)
 }
 int exact_tile_w(int n, int sem)
 {
-    if (sem != kSemLqr && n == 8) return kExPTW;
-    if (sem != kSemLqr) return n == 16 ? (kExPT / 64) * (64 - (n - 1)) : kEx8T;
+    if (sem != kSemLqr) return n == 8 ? kExPTW : (n == 16 ? kExP16TW : kEx8T);
     return n == 8 ? kEx8T : (n == 16 ? 64 : (kExST / 64) * (64 - (n - 1)));
 }
 int exact_default_tile_h(int n, int sem)
 {
+    if (sem != kSemLqr && n == 16) return 64;
     return (sem != kSemLqr && n == 8) ? kExPTT : DCTE_EX_TILE_H;
 }
 int exact_max_tile_h(int n, int sem)
 {
-    return (sem != kSemLqr && n == 8) ? kExPTT : (1 << 30);   // a lane per output row
+    if (sem != kSemLqr && n == 16) return 64;                  // a lane per output row
+    return (sem != kSemLqr && n == 8) ? kExPTT : (1 << 30);
 }
 
 hipError_t launch_map_exact(int n, int bpp, int sem, const MapParams& p, hipStream_t s)
