@@ -1022,10 +1022,19 @@ __device__ __forceinline__ bool rgb_line_grey(const uint32_t (&wd)[K])
 // (profiles/r04/memo_ab.jsonl).
 // 128 slots (8.7 KB with the queue, the block's LDS 11 KB: 3 waves per SIMD
 // still fit): vs 64 the grid 1.50 -> 1.39 ms, line art 0.269 -> 0.265, dots
-// -7 %; 256 costs occupancy (grid 1.62) (profiles/r04/memo_slots_ab.jsonl)
+// -7 %; 256 costs occupancy (grid 1.62) (profiles/r04/memo_slots_ab.jsonl).
+// Two ways (r05): a key may sit in its slot or the slot's pair partner (s ^ 1),
+// an empty way filled first; the 8-px grid (many distinct windows per slot)
+// 1.415 -> 1.18 ms at N = 8, line art and dots within +-1.5 %
+// (profiles/r05/memo_ways_ab.jsonl)
 #ifndef DCTE_MEMO_SLOTS
 #define DCTE_MEMO_SLOTS 128
 #endif
+#ifndef DCTE_MEMO_WAYS
+#define DCTE_MEMO_WAYS 2
+#endif
+constexpr int kMemoWays = DCTE_MEMO_WAYS;              // 1: direct-mapped; 2: slot pairs (s, s ^ 1)
+static_assert(kMemoWays == 1 || kMemoWays == 2, "memo ways");
 constexpr int kMemoSlots = DCTE_MEMO_SLOTS;            // a power of two
 static_assert((kMemoSlots & (kMemoSlots - 1)) == 0 && kMemoSlots >= 64, "memo slots");
 template <int N>
@@ -1158,6 +1167,12 @@ __device__ __forceinline__ void fix_dense_lane(const TileFixParams& tp, const do
             int s = 0;
             if (keyed) {
                 s = memo_slot(key);
+                if constexpr (kMemoWays == 2) {
+                    // an empty way first; both full: the way this lane's
+                    // position picks
+                    const bool f0 = memo[s * MS + KD] != kMemoEmpty, f1 = memo[(s ^ 1) * MS + KD] != kMemoEmpty;
+                    if (f0 && (!f1 || ((lane ^ y) & 1))) s ^= 1;
+                }
                 memo[s * MS + KD] = (uint32_t)lane;                 // one lane per slot wins
             }
             wave_sync_lds();
@@ -1296,11 +1311,20 @@ __device__ __forceinline__ void fix_dense_lane(const TileFixParams& tp, const do
                 align_rows(fv, foff, wa);
                 uint32_t key[KD];
                 if (act && make_key(wa, fast, key)) {
-                    const uint32_t* ent = memo + memo_slot(key) * MS;
-                    const uint32_t val = ent[KD];
+                    const int s0 = memo_slot(key);
+                    const uint32_t* ent = memo + s0 * MS;
+                    uint32_t val = ent[KD];
                     uint32_t diff = val == kMemoEmpty ? 1u : 0u;
 #pragma unroll
                     for (int j = 0; j < KD; j++) diff |= ent[j] ^ key[j];
+                    // the pair's other way (filled only after this one)
+                    if (kMemoWays == 2 && diff != 0u && val != kMemoEmpty) {
+                        ent = memo + (s0 ^ 1) * MS;
+                        val = ent[KD];
+                        diff = val == kMemoEmpty ? 1u : 0u;
+#pragma unroll
+                        for (int j = 0; j < KD; j++) diff |= ent[j] ^ key[j];
+                    }
                     if (diff == 0u) {
                         p.out[(long long)(y - p.y0) * p.out_stride + x] = __uint_as_float(val);
                         hit = true;
