@@ -40,6 +40,7 @@ KNOBS = {
     "DCTE_DENSE_OVERSUB": ("dcte_kernels.hip", "1"),
     "DCTE_DENSE_OVERSUB_MEMO": ("dcte_kernels.hip", "16"),
     "DCTE_MEMO_SLOTS": ("dcte_kernels.hip", "64"),
+    "DCTE_MEMO_WAYS": ("dcte_kernels.hip", "1"),
     "DCTE_EX_TILE_H": ("dcte_exact.hip", "64"),
     "DCTE_EX_MINW": ("dcte_exact.hip", "1"),
     "DCTE_EX16_MINW": ("dcte_exact.hip", "2"),
