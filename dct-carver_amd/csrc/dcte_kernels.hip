@@ -1025,7 +1025,8 @@ __device__ __forceinline__ bool rgb_line_grey(const uint32_t (&wd)[K])
 // -7 %; 256 costs occupancy (grid 1.62) (profiles/r04/memo_slots_ab.jsonl).
 // Two ways (r05): a key may sit in its slot or the slot's pair partner (s ^ 1),
 // an empty way filled first; the 8-px grid (many distinct windows per slot)
-// 1.415 -> 1.18 ms at N = 8, line art and dots within +-1.5 %
+// 1.415 -> 1.18 ms at N = 8, line art and dots within +-1.5 %; four ways
+// (s ^ 0 .. 3) 1.19
 // (profiles/r05/memo_ways_ab.jsonl)
 #ifndef DCTE_MEMO_SLOTS
 #define DCTE_MEMO_SLOTS 128
@@ -1033,8 +1034,8 @@ __device__ __forceinline__ bool rgb_line_grey(const uint32_t (&wd)[K])
 #ifndef DCTE_MEMO_WAYS
 #define DCTE_MEMO_WAYS 2
 #endif
-constexpr int kMemoWays = DCTE_MEMO_WAYS;              // 1: direct-mapped; 2: slot pairs (s, s ^ 1)
-static_assert(kMemoWays == 1 || kMemoWays == 2, "memo ways");
+constexpr int kMemoWays = DCTE_MEMO_WAYS;              // 1: direct-mapped; W: the slots s ^ 0 .. s ^ (W - 1)
+static_assert(kMemoWays == 1 || kMemoWays == 2 || kMemoWays == 4, "memo ways");
 constexpr int kMemoSlots = DCTE_MEMO_SLOTS;            // a power of two
 static_assert((kMemoSlots & (kMemoSlots - 1)) == 0 && kMemoSlots >= 64, "memo slots");
 template <int N>
@@ -1167,11 +1168,14 @@ __device__ __forceinline__ void fix_dense_lane(const TileFixParams& tp, const do
             int s = 0;
             if (keyed) {
                 s = memo_slot(key);
-                if constexpr (kMemoWays == 2) {
-                    // an empty way first; both full: the way this lane's
+                if constexpr (kMemoWays > 1) {
+                    // the first empty way; all full: the way this lane's
                     // position picks
-                    const bool f0 = memo[s * MS + KD] != kMemoEmpty, f1 = memo[(s ^ 1) * MS + KD] != kMemoEmpty;
-                    if (f0 && (!f1 || ((lane ^ y) & 1))) s ^= 1;
+                    int pick = -1;
+#pragma unroll
+                    for (int w = 0; w < kMemoWays; w++)
+                        if (pick < 0 && memo[(s ^ w) * MS + KD] == kMemoEmpty) pick = w;
+                    s ^= pick >= 0 ? pick : ((lane ^ y) & (kMemoWays - 1));
                 }
                 memo[s * MS + KD] = (uint32_t)lane;                 // one lane per slot wins
             }
@@ -1317,14 +1321,16 @@ __device__ __forceinline__ void fix_dense_lane(const TileFixParams& tp, const do
                     uint32_t diff = val == kMemoEmpty ? 1u : 0u;
 #pragma unroll
                     for (int j = 0; j < KD; j++) diff |= ent[j] ^ key[j];
-                    // the pair's other way (filled only after this one)
-                    if (kMemoWays == 2 && diff != 0u && val != kMemoEmpty) {
-                        ent = memo + (s0 ^ 1) * MS;
-                        val = ent[KD];
-                        diff = val == kMemoEmpty ? 1u : 0u;
+                    // the next ways (filled only after this one)
 #pragma unroll
-                        for (int j = 0; j < KD; j++) diff |= ent[j] ^ key[j];
-                    }
+                    for (int w = 1; w < kMemoWays; w++)
+                        if (diff != 0u && val != kMemoEmpty) {
+                            ent = memo + (s0 ^ w) * MS;
+                            val = ent[KD];
+                            diff = val == kMemoEmpty ? 1u : 0u;
+#pragma unroll
+                            for (int j = 0; j < KD; j++) diff |= ent[j] ^ key[j];
+                        }
                     if (diff == 0u) {
                         p.out[(long long)(y - p.y0) * p.out_stride + x] = __uint_as_float(val);
                         hit = true;
