@@ -921,6 +921,12 @@ __device__ __forceinline__ void refine_group(const double* lum, int LW, int at, 
 #ifndef DCTE_DENSE_OVERSUB_MEMO
 #define DCTE_DENSE_OVERSUB_MEMO 4
 #endif
+// N = 8 with the two-way memo (r05): 2 vs 4: line art 0.265 -> 0.251 ms, dots
+// -7 %, text -1 %, the grid +2 %; N = 4 keeps 4 (2: line art +7 %, dots +4 %)
+// (profiles/r05/memo_oversub_ab.jsonl)
+#ifndef DCTE_DENSE_OVERSUB_MEMO8
+#define DCTE_DENSE_OVERSUB_MEMO8 2
+#endif
 // grey layers at N <= 4 fit 128 VGPRs: 4 waves per SIMD (the LDS allows them)
 #ifndef DCTE_FIX_MINW
 #define DCTE_FIX_MINW 4
@@ -2470,7 +2476,8 @@ static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
         const long long most = kDenseFlat<N, SEM>
                                    ? ((long long)nstrips * 64 * p.m.tile_h + kDenseBatch16 - 1) / kDenseBatch16
                                    : nstrips;
-        const long long dmax = (long long)resident * (N <= 8 && BPP == 1 ? DCTE_DENSE_OVERSUB_MEMO : DCTE_DENSE_OVERSUB);
+        const long long dmax = (long long)resident * (N <= 8 && BPP == 1 ? (N == 8 ? DCTE_DENSE_OVERSUB_MEMO8 : DCTE_DENSE_OVERSUB_MEMO)
+                                                                     : DCTE_DENSE_OVERSUB);
         const int dblocks = (int)(most < dmax ? most : dmax);
         TileFixParams q = p;
         q.sparse_blocks = blocks;

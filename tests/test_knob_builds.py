@@ -39,6 +39,7 @@ KNOBS = {
     "DCTE_DENSE_CHUNK": ("dcte_kernels.hip", "8"),
     "DCTE_DENSE_OVERSUB": ("dcte_kernels.hip", "1"),
     "DCTE_DENSE_OVERSUB_MEMO": ("dcte_kernels.hip", "16"),
+    "DCTE_DENSE_OVERSUB_MEMO8": ("dcte_kernels.hip", "4"),
     "DCTE_MEMO_SLOTS": ("dcte_kernels.hip", "64"),
     "DCTE_MEMO_WAYS": ("dcte_kernels.hip", "1"),
     "DCTE_EX_TILE_H": ("dcte_exact.hip", "64"),
