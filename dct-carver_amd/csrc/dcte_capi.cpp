@@ -71,6 +71,8 @@ struct Device {
     size_t u8_cap = 0;
     uint8_t* d_tr = nullptr;       // transposed band (transposed maps)
     size_t tr_cap = 0;
+    float* d_out2 = nullptr;       // the transposed frame's map (dcte_energy_map2)
+    size_t out2_cap = 0;
     hipStream_t up = nullptr;      // host path: H2D copies
     hipStream_t down = nullptr;    // host path: D2H copies
     std::vector<hipEvent_t> ev;    // host path: chunk hand-offs
@@ -156,6 +158,27 @@ bool valid_n(int n) { return n == 2 || n == 4 || n == 8 || n == 16; }
 // does not compute in fp64 outright (seam bands and points; every map call
 // goes to dcte_exact.hip's sliding kernels)
 double eff_tau(const dcte_ctx* ctx) { return ctx->exact ? 1.0 : ctx->tie_tau; }
+
+// Runs a block of calls in a given arithmetic mode and restores the
+// context's own afterwards: a dcte_carver carries the mode it was created in
+// (DCTE_OPT_EXACT, DCTE_OPT_TIE_TAU), whatever the context was set to since.
+struct ModeScope {
+    dcte_ctx* ctx;
+    bool exact;
+    double tau;
+    ModeScope(dcte_ctx* c, bool e, double t) : ctx(c), exact(c->exact), tau(c->tie_tau)
+    {
+        c->exact = e;
+        c->tie_tau = t;
+    }
+    ~ModeScope()
+    {
+        ctx->exact = exact;
+        ctx->tie_tau = tau;
+    }
+    ModeScope(const ModeScope&) = delete;
+    ModeScope& operator=(const ModeScope&) = delete;
+};
 
 // window offsets -hl .. +hr of a semantics
 void halo(int n, int sem, int& hl, int& hr)
@@ -347,6 +370,9 @@ int run_exact(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, i
         ctx->fail_inject = 0;
         return hip_fail(ctx, hipErrorLaunchFailure, "launch_map_exact (injected)");
     }
+    // an armed refinement-launch failure (2) is consumed here: this call has no
+    // refinement launch, and it must not fire in a later fast-mode call
+    if (ctx->fail_inject == 2) ctx->fail_inject = 0;
     return DCTE_OK;
 }
 
@@ -583,6 +609,24 @@ int ensure_pipe(dcte_ctx* ctx, Device& d, size_t nev)
     return DCTE_OK;
 }
 
+// Zeroes the refined-pixel counter of the host path's stream before a band's
+// launches (sync_bands reads it).  The exact mode has no refinement lists, so
+// only a fast-mode call grows them to the band's size.
+int reset_refined(dcte_ctx* ctx, Device& d, int w, int rows, int n, int sem)
+{
+    FixScratch* f = nullptr;
+    if (!(ctx->exact && dcte::exact_supported(n, sem))) {
+        int rc = ensure_fix(ctx, d, d.stream, (size_t)w * (size_t)rows, &f);
+        if (rc) return rc;
+    } else {
+        auto it = d.fix.find(d.stream);
+        if (it == d.fix.end()) return DCTE_OK;
+        f = &it->second;
+    }
+    DCTE_HIP(ctx, hipMemsetAsync(f->d_count + 1, 0, sizeof(unsigned), d.stream));
+    return DCTE_OK;
+}
+
 // host frame -> device band maps (rows split over the context's devices),
 // left on the devices in d.d_out; returns the number of devices used.
 // Each band runs as a pipeline of row chunks on three streams -- H2D of the
@@ -614,10 +658,8 @@ int map_bands(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t ro
         if (rc) return rc;
         rc = ensure_buf(ctx, (void**)&d.d_out, &d.out_cap, out_bytes);
         if (rc) return rc;
-        FixScratch* f = nullptr;
-        rc = ensure_fix(ctx, d, d.stream, (size_t)W * (size_t)(y1 - y0), &f);
+        rc = reset_refined(ctx, d, W, y1 - y0, n, sem);
         if (rc) return rc;
-        DCTE_HIP(ctx, hipMemsetAsync(f->d_count + 1, 0, sizeof(unsigned), d.stream));
         if (transposed) {
             // source columns [lo, hi] of all h rows -> (h x cols) strip -> transpose
             const size_t sw = (size_t)(hi - lo + 1) * bpp;
@@ -669,6 +711,86 @@ int map_bands(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t ro
                                              hipMemcpyDeviceToHost, d.down));
             }
         }
+    }
+    return DCTE_OK;
+}
+
+// Host path on ONE device with the whole frame resident (the
+// plug-in's build for a vertical resize needs the maps of both orientations,
+// src/render.c:358-364): row chunks of the frame go up on d.up; with `out`,
+// each chunk is mapped on d.stream as soon as its rows and halo are in and its
+// map goes down on d.down; with `out_t`, the resident frame is then
+// transposed in HBM and the transposed frame mapped in row chunks (= source
+// column strips), each downloaded as soon as it is mapped -- one upload for
+// both orientations, and the downloads of both maps back to back on d.down.
+int map_pipeline_one(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride,
+                     int n, float edges, float textures, int sem, float* out, float* out_t)
+{
+    Device& d = ctx->devs[0];
+    int hl, hr;
+    halo(n, sem, hl, hr);
+    const size_t pitch = (size_t)w * bpp, pitch_t = (size_t)h * bpp;
+    const size_t fbytes = pitch * (size_t)h, mbytes = sizeof(float) * (size_t)w * (size_t)h;
+    int rc = ensure_stream(ctx, d);
+    if (rc) return rc;
+    if ((rc = ensure_buf(ctx, (void**)&d.d_in, &d.in_cap, fbytes))) return rc;
+    if (out && (rc = ensure_buf(ctx, (void**)&d.d_out, &d.out_cap, mbytes))) return rc;
+    if (out_t) {
+        if ((rc = ensure_buf(ctx, (void**)&d.d_tr, &d.tr_cap, fbytes))) return rc;
+        if ((rc = ensure_buf(ctx, (void**)&d.d_out2, &d.out2_cap, mbytes))) return rc;
+    }
+    if ((rc = reset_refined(ctx, d, w, h, n, sem))) return rc;
+    // at least 8 chunks of >= 256 rows where the frame allows (map_bands)
+    auto chunks = [](int rows) {
+        int crows = rows / 8;
+        crows = crows < 256 ? 256 : (crows > kChunkRows ? kChunkRows : crows);
+        int nch = (rows + crows - 1) / crows;
+        return nch < 1 ? 1 : (nch > kMaxChunks ? kMaxChunks : nch);
+    };
+    const int nch0 = chunks(h), nch1 = out_t ? chunks(w) : 0;
+    if ((rc = ensure_pipe(ctx, d, 2 * (size_t)nch0 + (size_t)nch1))) return rc;
+    int loaded = -1;                                            // last uploaded row
+    for (int c = 0; c < nch0; c++) {
+        const int a = (int)((long long)h * c / nch0), b = (int)((long long)h * (c + 1) / nch0);
+        if (a == b) continue;
+        const int need = out ? (b - 1 + hr < h - 1 ? b - 1 + hr : h - 1) : b - 1;
+        hipEvent_t ev_up = d.ev[2 * c], ev_map = d.ev[2 * c + 1];
+        if (need > loaded) {
+            DCTE_HIP(ctx, hipMemcpy2DAsync(d.d_in + (size_t)(loaded + 1) * pitch, pitch,
+                                           px + (size_t)(loaded + 1) * rowstride, rowstride, pitch,
+                                           need - loaded, hipMemcpyHostToDevice, d.up));
+            loaded = need;
+        }
+        DCTE_HIP(ctx, hipEventRecord(ev_up, d.up));
+        if (!out) continue;
+        DCTE_HIP(ctx, hipStreamWaitEvent(d.stream, ev_up, 0));
+        rc = run_device(ctx, d, d.d_in, (long long)pitch, w, h, bpp, 0, loaded + 1, a, b, n, edges,
+                        textures, sem, d.d_out + (size_t)a * w, w, d.stream);
+        if (rc) return rc;
+        DCTE_HIP(ctx, hipEventRecord(ev_map, d.stream));
+        DCTE_HIP(ctx, hipStreamWaitEvent(d.down, ev_map, 0));
+        DCTE_HIP(ctx, hipMemcpyAsync(out + (size_t)a * w, d.d_out + (size_t)a * w,
+                                     sizeof(float) * (size_t)w * (size_t)(b - a),
+                                     hipMemcpyDeviceToHost, d.down));
+    }
+    if (!out_t) return DCTE_OK;
+    // the whole frame is in once the last upload is (ordered after every copy on d.up)
+    DCTE_HIP(ctx, hipEventRecord(d.ev[2 * nch0 - 2], d.up));
+    DCTE_HIP(ctx, hipStreamWaitEvent(d.stream, d.ev[2 * nch0 - 2], 0));
+    DCTE_HIP(ctx, dcte::launch_transpose_u8(d.d_in, (long long)pitch, h, w, bpp, d.d_tr,
+                                            (long long)pitch_t, d.stream));
+    for (int c = 0; c < nch1; c++) {
+        const int a = (int)((long long)w * c / nch1), b = (int)((long long)w * (c + 1) / nch1);
+        if (a == b) continue;
+        rc = run_device(ctx, d, d.d_tr, (long long)pitch_t, h, w, bpp, 0, w, a, b, n, edges, textures,
+                        sem, d.d_out2 + (size_t)a * h, h, d.stream);
+        if (rc) return rc;
+        hipEvent_t ev_map = d.ev[2 * nch0 + c];
+        DCTE_HIP(ctx, hipEventRecord(ev_map, d.stream));
+        DCTE_HIP(ctx, hipStreamWaitEvent(d.down, ev_map, 0));
+        DCTE_HIP(ctx, hipMemcpyAsync(out_t + (size_t)a * h, d.d_out2 + (size_t)a * h,
+                                     sizeof(float) * (size_t)h * (size_t)(b - a),
+                                     hipMemcpyDeviceToHost, d.down));
     }
     return DCTE_OK;
 }
@@ -762,6 +884,7 @@ void dcte_destroy(dcte_ctx* ctx)
         if (d.d_keys) (void)hipFree(d.d_keys);
         if (d.d_u8) (void)hipFree(d.d_u8);
         if (d.d_tr) (void)hipFree(d.d_tr);
+        if (d.d_out2) (void)hipFree(d.d_out2);
         if (d.up) (void)hipStreamSynchronize(d.up);
         if (d.down) (void)hipStreamSynchronize(d.down);
         for (hipEvent_t e : d.ev) (void)hipEventDestroy(e);
@@ -1248,6 +1371,8 @@ struct dcte_carver {
     dcte_ctx* ctx = nullptr;
     int W0 = 0, H = 0, w = 0, bpp = 0, n = 0, r = 0, bw = 0;
     float edges = 0, textures = 0;
+    bool exact = false;        // DCTE_OPT_EXACT when the carver was created
+    double tie_tau = 0;        // DCTE_OPT_TIE_TAU likewise
     size_t pitch = 0;
     uint8_t* d_px = nullptr;   // carved frame (row pitch W0 * bpp)
     float* d_map = nullptr;    // its energies (row pitch W0)
@@ -1276,9 +1401,9 @@ void carver_free(dcte_carver* c)
 
 extern "C" {
 
-int dcte_carver_create(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride,
-                       int n, float edges, float textures, int transposed, float* map_out,
-                       dcte_carver** out)
+int dcte_carver_create2(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride,
+                        int n, float edges, float textures, int transposed, float* map_out,
+                        float* map_other_out, dcte_carver** out)
 {
     DeviceGuard guard_;
     if (!ctx || !out) return DCTE_EINVAL;
@@ -1301,48 +1426,81 @@ int dcte_carver_create(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, 
     c->bw = 8 * c->r + 4;            // reading windows of the update band too (dcte_band_gather)
     c->edges = edges;
     c->textures = textures;
+    c->exact = ctx->exact;           // the carver keeps this mode for every step
+    c->tie_tau = ctx->tie_tau;
     c->pitch = (size_t)c->W0 * bpp;
     c->seam.assign(c->H, 0);
     const size_t fbytes = c->pitch * (size_t)c->H;
+    const size_t mbytes = sizeof(float) * (size_t)w * (size_t)h;
+    uint8_t* d_tmp = nullptr;        // the other orientation's frame
+    float* d_other = nullptr;        // its map
+    auto release_tmp = [&]() {
+        if (d_tmp || d_other) (void)hipStreamSynchronize(s);
+        if (d_tmp) (void)hipFree(d_tmp);
+        if (d_other) (void)hipFree(d_other);
+        d_tmp = nullptr;
+        d_other = nullptr;
+    };
     auto fail = [&](hipError_t e, const char* where) {
         int code = hip_fail(ctx, e, where);
+        release_tmp();
         carver_free(c);
         return code;
     };
     hipError_t e;
     if ((e = hipMalloc(&c->d_px, fbytes)) != hipSuccess) return fail(e, "hipMalloc frame");
-    if ((e = hipMalloc(&c->d_map, sizeof(float) * (size_t)c->W0 * c->H)) != hipSuccess) return fail(e, "hipMalloc map");
+    if ((e = hipMalloc(&c->d_map, mbytes)) != hipSuccess) return fail(e, "hipMalloc map");
     if ((e = hipMalloc(&c->d_seam, sizeof(int) * (size_t)c->H)) != hipSuccess) return fail(e, "hipMalloc seam");
     if ((e = hipMalloc(&c->d_x0, sizeof(int) * (size_t)c->H)) != hipSuccess) return fail(e, "hipMalloc x0");
     if ((e = hipMalloc(&c->d_be, sizeof(float) * (size_t)c->H * c->bw)) != hipSuccess) return fail(e, "hipMalloc band");
     if ((e = hipMalloc(&c->d_bpx, (size_t)c->H * c->bw * bpp)) != hipSuccess) return fail(e, "hipMalloc band px");
     const size_t spitch = (size_t)w * bpp;
-    if (transposed) {
-        uint8_t* d_tmp = nullptr;
+    if (transposed || map_other_out)
         if ((e = hipMalloc(&d_tmp, fbytes)) != hipSuccess) return fail(e, "hipMalloc staging");
+    if (map_other_out && (e = hipMalloc(&d_other, mbytes)) != hipSuccess) return fail(e, "hipMalloc other map");
+    // one upload: the frame as given, or (transposed) into the staging buffer
+    // and transposed from there; the other orientation is the staging frame
+    // (transposed) or the frame transposed into it
+    if (transposed) {
         e = hipMemcpy2DAsync(d_tmp, spitch, px, rowstride, spitch, h, hipMemcpyHostToDevice, s);
         if (e == hipSuccess)
             e = dcte::launch_transpose_u8(d_tmp, (long long)spitch, h, w, bpp, c->d_px, (long long)c->pitch, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        (void)hipFree(d_tmp);
         if (e != hipSuccess) return fail(e, "upload (transposed)");
-    } else if ((e = hipMemcpy2DAsync(c->d_px, c->pitch, px, rowstride, spitch, h,
-                                     hipMemcpyHostToDevice, s)) != hipSuccess) {
-        return fail(e, "upload");
+    } else {
+        e = hipMemcpy2DAsync(c->d_px, c->pitch, px, rowstride, spitch, h, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess && map_other_out)
+            e = dcte::launch_transpose_u8(c->d_px, (long long)c->pitch, h, w, bpp, d_tmp, (long long)h * bpp, s);
+        if (e != hipSuccess) return fail(e, "upload");
     }
     rc = run_device(ctx, d, c->d_px, (long long)c->pitch, c->W0, c->H, bpp, 0, c->H, 0, c->H, n,
                     edges, textures, DCTE_LQR, c->d_map, c->W0, s);
     if (rc == DCTE_OK && map_out &&
-        (e = hipMemcpyAsync(map_out, c->d_map, sizeof(float) * (size_t)c->W0 * c->H,
-                            hipMemcpyDeviceToHost, s)) != hipSuccess)
+        (e = hipMemcpyAsync(map_out, c->d_map, mbytes, hipMemcpyDeviceToHost, s)) != hipSuccess)
         rc = hip_fail(ctx, e, "map download");
+    if (rc == DCTE_OK && map_other_out) {
+        const int ow = c->H, oh = c->W0;      // the other orientation's frame: ow x oh
+        rc = run_device(ctx, d, d_tmp, (long long)ow * bpp, ow, oh, bpp, 0, oh, 0, oh, n, edges,
+                        textures, DCTE_LQR, d_other, ow, s);
+        if (rc == DCTE_OK &&
+            (e = hipMemcpyAsync(map_other_out, d_other, mbytes, hipMemcpyDeviceToHost, s)) != hipSuccess)
+            rc = hip_fail(ctx, e, "other map download");
+    }
     if (rc == DCTE_OK && (e = hipStreamSynchronize(s)) != hipSuccess) rc = hip_fail(ctx, e, "sync");
+    release_tmp();
     if (rc) {
         carver_free(c);
         return rc;
     }
     *out = c;
     return DCTE_OK;
+}
+
+int dcte_carver_create(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride,
+                       int n, float edges, float textures, int transposed, float* map_out,
+                       dcte_carver** out)
+{
+    return dcte_carver_create2(ctx, px, w, h, bpp, rowstride, n, edges, textures, transposed,
+                               map_out, nullptr, out);
 }
 
 int dcte_carver_width(const dcte_carver* c) { return c ? c->w : 0; }
@@ -1359,6 +1517,7 @@ int dcte_carver_step(dcte_carver* c, int* seam, int* band_x0, float* band_e, uin
     int rc = ensure_stream(ctx, d);
     if (rc) return rc;
     hipStream_t s = d.stream;
+    ModeScope mode(ctx, c->exact, c->tie_tau);   // the carver's mode, not the context's now
     // the seam first, checked on the host before anything moves (a search
     // that timed out is re-run band-wise, as dcte_seam_find does)
     for (;;) {
@@ -1426,13 +1585,46 @@ int dcte_energy_map(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, siz
     HostPin pin_in(ctx, px, (size_t)(h - 1) * rowstride + (size_t)w * bpp);
     HostPin pin_out(ctx, out, sizeof(float) * (size_t)w * (size_t)h);
     int G = 0;
-    int rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, transposed,
-                       out, &G);
+    int rc;
+    if (transposed && ctx->devs.size() == 1) {   // chunked: the map's download overlaps its launches
+        G = 1;
+        rc = map_pipeline_one(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, nullptr, out);
+    } else {
+        rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, transposed, out, &G);
+    }
     if (rc) {
         drain(ctx, G);              // nothing in flight may still use px / out
         return rc;
     }
     return sync_bands(ctx, G);
+}
+
+int dcte_energy_map2(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride,
+                     int n, float edges, float textures, int semantics, float* out, float* out_t)
+{
+    DeviceGuard guard_;
+    if (!ctx) return DCTE_EINVAL;
+    DCTE_ARG(ctx, px && (out || out_t) && valid_n(n) && valid_sem_bpp(semantics, bpp) && w > 0 && h > 0);
+    DCTE_ARG(ctx, rowstride >= (size_t)w * bpp);
+    if (ctx->devs.size() > 1) {     // row bands per device: one call per orientation
+        int rc = out ? dcte_energy_map(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, 0, out)
+                     : DCTE_OK;
+        long long refined = ctx->last_refined;
+        if (rc == DCTE_OK && out_t)
+            rc = dcte_energy_map(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, 1, out_t);
+        ctx->last_refined += refined;
+        return rc;
+    }
+    ctx->last_refined = 0;
+    HostPin pin_in(ctx, px, (size_t)(h - 1) * rowstride + (size_t)w * bpp);
+    HostPin pin_out(ctx, out, out ? sizeof(float) * (size_t)w * (size_t)h : 0);
+    HostPin pin_out_t(ctx, out_t, out_t ? sizeof(float) * (size_t)w * (size_t)h : 0);
+    int rc = map_pipeline_one(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, out, out_t);
+    if (rc) {
+        drain(ctx, 1);              // nothing in flight may still use px / out / out_t
+        return rc;
+    }
+    return sync_bands(ctx, 1);
 }
 
 int dcte_energy_image_u8(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp,

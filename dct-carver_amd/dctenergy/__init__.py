@@ -53,7 +53,8 @@ EXPORTS = ("dcte_abi_version", "dcte_device_count", "dcte_create", "dcte_destroy
            "dcte_carve", "dcte_energy_windows", "dcte_energy_windows_device",
            "dcte_energy_window", "dcte_normalize_u8_host", "dcte_carver_create",
            "dcte_carver_step", "dcte_carver_width", "dcte_carver_height",
-           "dcte_carver_band_width", "dcte_carver_destroy")
+           "dcte_carver_band_width", "dcte_carver_destroy", "dcte_energy_map2",
+           "dcte_carver_create2")
 
 _lib = None
 
@@ -111,6 +112,10 @@ def lib():
     L.dcte_energy_map.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                   ctypes.c_size_t, ctypes.c_int, ctypes.c_float,
                                   ctypes.c_float, ctypes.c_int, ctypes.c_int, vp]
+    L.dcte_energy_map2.restype = ctypes.c_int
+    L.dcte_energy_map2.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_size_t, ctypes.c_int, ctypes.c_float,
+                                   ctypes.c_float, ctypes.c_int, vp, vp]
     L.dcte_energy_map_device.restype = ctypes.c_int
     L.dcte_energy_map_device.argtypes = [vp, ctypes.c_int, vp, ctypes.c_longlong, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -164,6 +169,9 @@ def lib():
     L.dcte_carver_create.restype = i
     L.dcte_carver_create.argtypes = [vp, vp, i, i, i, ctypes.c_size_t, i, f, f, i, vp,
                                      ctypes.POINTER(vp)]
+    L.dcte_carver_create2.restype = i
+    L.dcte_carver_create2.argtypes = [vp, vp, i, i, i, ctypes.c_size_t, i, f, f, i, vp, vp,
+                                      ctypes.POINTER(vp)]
     L.dcte_carver_step.restype = i
     L.dcte_carver_step.argtypes = [vp, vp, vp, vp, vp]
     for fn in ("dcte_carver_width", "dcte_carver_height", "dcte_carver_band_width"):
@@ -270,9 +278,9 @@ class Context:
         return n.value, ms.value
 
     # -- host entry point
-    def energy_map(self, px, n=8, edges=0.5, textures=0.5, semantics=DCTE_LQR,
-                   transposed=False, out=None):
-        """Energy map of an HxW (grey) or HxWxC uint8 frame -> HxW float32."""
+    @staticmethod
+    def _frame(px):
+        """-> (px as a uint8 array with packed pixels, h, w, bpp, rowstride)"""
         px = np.asarray(px)
         if px.dtype != np.uint8:
             raise TypeError("px must be uint8")
@@ -285,16 +293,39 @@ class Context:
             raise ValueError("px must be HxW or HxWxC")
         if px.strides[-1] != 1 or (px.ndim == 3 and px.strides[1] != bpp):
             px = np.ascontiguousarray(px)
-        rowstride = _rowstride(px)
-        shape = (w, h) if transposed else (h, w)
+        return px, h, w, bpp, _rowstride(px)
+
+    @staticmethod
+    def _out(out, shape):
         if out is None:
-            out = np.empty(shape, np.float32)
-        elif out.shape != shape or out.dtype != np.float32 or not out.flags.c_contiguous:
+            return np.empty(shape, np.float32)
+        if out.shape != shape or out.dtype != np.float32 or not out.flags.c_contiguous:
             raise ValueError(f"out must be a C-contiguous {shape} float32 array")
+        return out
+
+    def energy_map(self, px, n=8, edges=0.5, textures=0.5, semantics=DCTE_LQR,
+                   transposed=False, out=None):
+        """Energy map of an HxW (grey) or HxWxC uint8 frame -> HxW float32."""
+        px, h, w, bpp, rowstride = self._frame(px)
+        out = self._out(out, (w, h) if transposed else (h, w))
         self._check(lib().dcte_energy_map(self._h, px.ctypes.data, w, h, bpp, rowstride, n,
                                           edges, textures, semantics, int(bool(transposed)),
                                           out.ctypes.data))
         return out
+
+    def energy_map2(self, px, n=8, edges=0.5, textures=0.5, semantics=DCTE_LQR, out=None,
+                    out_t=None, want=(True, True)):
+        """Both orientations from one upload (dcte_energy_map2): -> (HxW map,
+        WxH map of the transposed frame); want = which of the two to compute
+        (None in its place when not)."""
+        px, h, w, bpp, rowstride = self._frame(px)
+        o = self._out(out, (h, w)) if want[0] else None
+        ot = self._out(out_t, (w, h)) if want[1] else None
+        self._check(lib().dcte_energy_map2(self._h, px.ctypes.data, w, h, bpp, rowstride, n,
+                                           edges, textures, semantics,
+                                           o.ctypes.data if o is not None else None,
+                                           ot.ctypes.data if ot is not None else None))
+        return o, ot
 
     # -- energy image as 8-bit grey (SURVEY §8a-a11)
     def normalize_u8(self, E, mode=DCTE_NORM_PREVIEW, channels=1):
@@ -448,17 +479,27 @@ class Context:
         return out
 
     # -- device mirror of a liblqr carver (the update_emap hook)
-    def carver(self, px, n=8, edges=0.5, textures=0.5, transposed=False):
-        """-> (Carver, first map of the mirrored frame)."""
+    def carver(self, px, n=8, edges=0.5, textures=0.5, transposed=False, other=False):
+        """-> (Carver, first map of the mirrored frame); other=True
+        (dcte_carver_create2): -> (Carver, first map, map of the other
+        orientation) from the same upload.  The carver keeps the context's
+        arithmetic mode of this moment (DCTE_OPT_EXACT / DCTE_OPT_TIE_TAU)."""
         px = np.ascontiguousarray(px, dtype=np.uint8)
         h, w = px.shape[:2]
         bpp = 1 if px.ndim == 2 else px.shape[2]
         first = np.empty((w, h) if transposed else (h, w), np.float32)
         c = ctypes.c_void_p()
-        self._check(lib().dcte_carver_create(self._h, px.ctypes.data, w, h, bpp, _rowstride(px), n,
-                                             edges, textures, int(bool(transposed)),
-                                             first.ctypes.data, ctypes.byref(c)))
-        return Carver(self, c, bpp), first
+        if not other:
+            self._check(lib().dcte_carver_create(self._h, px.ctypes.data, w, h, bpp, _rowstride(px),
+                                                 n, edges, textures, int(bool(transposed)),
+                                                 first.ctypes.data, ctypes.byref(c)))
+            return Carver(self, c, bpp), first
+        second = np.empty((h, w) if transposed else (w, h), np.float32)
+        self._check(lib().dcte_carver_create2(self._h, px.ctypes.data, w, h, bpp, _rowstride(px), n,
+                                              edges, textures, int(bool(transposed)),
+                                              first.ctypes.data, second.ctypes.data,
+                                              ctypes.byref(c)))
+        return Carver(self, c, bpp), first, second
 
     # -- minimum-energy seam (SURVEY §8f-4)
     def seam_find(self, E):

@@ -12,7 +12,11 @@
 #include "dctenergy.h"
 
 static dcte_ctx *g_ctx;
-static int g_ctx_status = 1; /* 1 = not tried yet */
+static int g_ctx_status = DCTE_ENODEV;
+static pthread_once_t g_ctx_once = PTHREAD_ONCE_INIT;
+/* the glue's calls on the shared context: an option set and the call it is
+ * meant for must not interleave with another thread's */
+static pthread_mutex_t g_ctx_lock = PTHREAD_MUTEX_INITIALIZER;
 
 static void release_ctx(void)
 {
@@ -20,14 +24,27 @@ static void release_ctx(void)
     g_ctx = NULL;
 }
 
+static void create_ctx(void)
+{
+    const char *ng = getenv("DCTE_NGPUS");
+    g_ctx_status = dcte_create(&g_ctx, ng && *ng ? atoi(ng) : 1, 0);
+    if (g_ctx_status == DCTE_OK) atexit(release_ctx);
+}
+
+/* created once per process, whichever thread asks first */
 static dcte_ctx *plugin_ctx(void)
 {
-    if (g_ctx_status == 1) {
-        const char *ng = getenv("DCTE_NGPUS");
-        g_ctx_status = dcte_create(&g_ctx, ng && *ng ? atoi(ng) : 1, 0);
-        if (g_ctx_status == DCTE_OK) atexit(release_ctx);
-    }
+    pthread_once(&g_ctx_once, create_ctx);
     return g_ctx_status == DCTE_OK ? g_ctx : NULL;
+}
+
+/* the arithmetic a glue call runs in (DCTE_PLUGIN_EXACT), set on the shared
+ * context right before the call under g_ctx_lock; a carver mirror keeps the
+ * mode it was created in (dcte_carver_create), so later calls of another
+ * mode do not reach it */
+static int set_mode(dcte_ctx *ctx, unsigned flags)
+{
+    return dcte_set_option(ctx, DCTE_OPT_EXACT, (flags & DCTE_PLUGIN_EXACT) ? 1.0 : 0.0);
 }
 
 static void release_hook(dcte_map_cache *c)
@@ -52,22 +69,24 @@ int dcte_plugin_build_ex(dcte_map_cache *c, const uint8_t *px, int w, int h, int
 {
     if (!c) return DCTE_EINVAL;
     memset(c, 0, sizeof(*c));
+    c->flags = flags;
     dcte_ctx *ctx = plugin_ctx();
     if (!ctx) return c->status = g_ctx_status;
     if (w <= 0 || h <= 0) return c->status = DCTE_EINVAL;
-    /* the process-wide context follows the latest build's mode */
-    if (dcte_set_option(ctx, DCTE_OPT_EXACT, (flags & DCTE_PLUGIN_EXACT) ? 1.0 : 0.0) != DCTE_OK)
-        return c->status = DCTE_EINVAL;
-    c->map = (float *)malloc(sizeof(float) * (size_t)w * (size_t)h);
-    if (!c->map) return c->status = DCTE_ENOMEM;
+    pthread_mutex_lock(&g_ctx_lock);
+    int st = set_mode(ctx, flags);
+    const size_t npx = (size_t)w * (size_t)h;
     const int ho = with_transposed ? 1 : 0;
-    if ((flags & DCTE_PLUGIN_SEAM_HOOK) && (bpp == 1 || bpp == 3)) {
-        /* the mirror maps the frame of the resize orientation itself */
-        float *first = NULL;
-        if (ho) first = c->map_t = (float *)malloc(sizeof(float) * (size_t)w * (size_t)h);
-        else first = c->map;
-        if (first && dcte_carver_create(ctx, px, w, h, bpp, rowstride, blocksize, edges, textures, ho,
-                                        first, &c->mirror) == DCTE_OK) {
+    if (st == DCTE_OK) {
+        c->map = (float *)malloc(sizeof(float) * npx);
+        if (ho) c->map_t = (float *)malloc(sizeof(float) * npx);
+        if (!c->map || (ho && !c->map_t)) st = DCTE_ENOMEM;
+    }
+    if (st == DCTE_OK && (flags & DCTE_PLUGIN_SEAM_HOOK) && (bpp == 1 || bpp == 3)) {
+        /* the mirror maps the frame of the resize orientation itself, and the
+         * other orientation's map from the same upload */
+        if (dcte_carver_create2(ctx, px, w, h, bpp, rowstride, blocksize, edges, textures, ho,
+                                ho ? c->map_t : c->map, ho ? c->map : NULL, &c->mirror) == DCTE_OK) {
             c->hook_orientation = ho;
             c->n = blocksize;
             c->mw = dcte_carver_width(c->mirror);
@@ -79,36 +98,45 @@ int dcte_plugin_build_ex(dcte_map_cache *c, const uint8_t *px, int w, int h, int
             c->band_px = (unsigned char *)malloc((size_t)c->mh * c->bw * bpp);
             c->ver_lo = (int *)malloc(sizeof(int) * (size_t)c->mh);
             c->ver_hi = (int *)malloc(sizeof(int) * (size_t)c->mh);
+            c->last_x = -1;
             c->hook_ok = c->band_x0 && c->band_e && c->band_px && c->ver_lo && c->ver_hi;
             if (!c->hook_ok) release_hook(c);
         }
-        if (!c->mirror && ho) {           /* no mirror: the map_t build below */
-            free(c->map_t);
-            c->map_t = NULL;
-        }
     }
-    c->status = DCTE_OK;
-    if (!(c->mirror && ho == 0))
-        c->status = dcte_energy_map(ctx, px, w, h, bpp, rowstride, blocksize, edges, textures,
-                                    DCTE_LQR, 0, c->map);
-    if (c->status == DCTE_OK && with_transposed && !c->map_t) {
-        c->map_t = (float *)malloc(sizeof(float) * (size_t)w * (size_t)h);
-        c->status = c->map_t ? dcte_energy_map(ctx, px, w, h, bpp, rowstride, blocksize, edges,
-                                               textures, DCTE_LQR, 1, c->map_t)
-                             : DCTE_ENOMEM;
-    }
-    if (c->status != DCTE_OK) {
-        int st = c->status;
+    /* no mirror (no hook, or it could not be set up): both maps from one
+     * upload, dcte_energy_map2 */
+    if (st == DCTE_OK && !c->mirror)
+        st = dcte_energy_map2(ctx, px, w, h, bpp, rowstride, blocksize, edges, textures, DCTE_LQR,
+                              c->map, c->map_t);
+    pthread_mutex_unlock(&g_ctx_lock);
+    if (st != DCTE_OK) {
         release_hook(c);
         free(c->map);
         free(c->map_t);
         memset(c, 0, sizeof(*c));
         return c->status = st;
     }
+    c->status = DCTE_OK;
     c->w = w;
     c->h = h;
     c->valid = 1;
     return DCTE_OK;
+}
+
+int dcte_plugin_preview_u8(const uint8_t *region, int w, int h, int channels, int blocksize,
+                           float edges, float textures, unsigned flags, uint8_t *out)
+{
+    dcte_ctx *ctx = plugin_ctx();
+    if (!ctx) return g_ctx_status;
+    if (!region || !out || w <= 0 || h <= 0) return DCTE_EINVAL;
+    pthread_mutex_lock(&g_ctx_lock);
+    int st = set_mode(ctx, flags);
+    if (st == DCTE_OK)
+        st = dcte_energy_image_u8(ctx, region, w, h, channels, (size_t)w * (size_t)channels,
+                                  blocksize, edges, textures, DCTE_PREVIEW, DCTE_NORM_PREVIEW,
+                                  channels, out);
+    pthread_mutex_unlock(&g_ctx_lock);
+    return st;
 }
 
 int dcte_plugin_build(dcte_map_cache *c, const uint8_t *px, int w, int h, int bpp,
@@ -223,7 +251,10 @@ int dcte_plugin_lookup_hook(dcte_map_cache *c, int x, int y, int w, int h, int o
         return 0;
     /* liblqr carved since the mirror's last step: carve as many seams */
     while (w < c->mw) {
-        if (dcte_carver_step(c->mirror, NULL, c->band_x0, c->band_e, c->band_px) != DCTE_OK) {
+        pthread_mutex_lock(&g_ctx_lock);
+        const int st = dcte_carver_step(c->mirror, NULL, c->band_x0, c->band_e, c->band_px);
+        pthread_mutex_unlock(&g_ctx_lock);
+        if (st != DCTE_OK) {
             release_hook(c);
             c->missed++;
             return 0;
@@ -232,12 +263,17 @@ int dcte_plugin_lookup_hook(dcte_map_cache *c, int x, int y, int w, int h, int o
         c->steps++;
         c->band_valid = 1;
         reset_checked(c);                          /* nothing of the new band checked yet */
+        c->last_y = 0;
+        c->last_x = -1;
     }
     /* liblqr walks a pass (an update or a rebuild of its energy map) in
-     * increasing rows: a callback above the previous one starts another pass,
-     * and liblqr's image may have changed since the columns were checked */
-    if (y < c->last_y) reset_checked(c);
+     * increasing rows, and along a row in increasing columns: a callback above
+     * the previous one, or on its row but not to the right of it, starts
+     * another pass, and liblqr's image may have changed since the columns
+     * were checked */
+    if (y < c->last_y || (y == c->last_y && x <= c->last_x)) reset_checked(c);
     c->last_y = y;
+    c->last_x = x;
     const int chk = dcte_plugin_window_check(c, x, y, w, h, rd, rw);
     const int k = chk == 1 ? x - c->band_x0[y] : -1;
     if (chk <= 0 || k < 0 || k >= c->bw) {

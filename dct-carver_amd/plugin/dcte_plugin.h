@@ -29,6 +29,7 @@ typedef struct {
     int w, h;        /* frame size */
     int valid;
     int status;      /* DCTE_* code of the last build */
+    unsigned flags;  /* the build's DCTE_PLUGIN_* flags: this carver's mode */
     /* opt-in seam hook (DCTE_PLUGIN_SEAM_HOOK): a device
      * mirror of the carver that replays each seam liblqr carves and hands
      * back the energies and pixels around it, so update_emap's callbacks are
@@ -44,22 +45,28 @@ typedef struct {
     float *band_e;         /* mh x bw energies of the last step's band */
     unsigned char *band_px;/* mh x bw x bpp pixels of the carved frame (window check) */
     int *ver_lo, *ver_hi;  /* mh: columns of each row already checked against liblqr this pass */
-    int last_y;            /* row of the previous hooked callback: a lower one starts a new pass */
+    int last_y, last_x;    /* the previous hooked callback: one above it, or on its row and not
+                              right of it, starts a new pass */
     long long served_band, missed, out_of_band, steps, reads;
 } dcte_map_cache;
 
 #define DCTE_PLUGIN_SEAM_HOOK 1u
 /* every energy the plug-in serves is the reference's own double: the maps and
  * the hook's band updates in the exact mode (DCTE_OPT_EXACT), so liblqr carves
- * the reference's seams */
+ * the reference's seams.  The mode belongs to the cache it was built with: a
+ * later build or preview in the other mode (the dialog's preview, a second
+ * carver, src/interface.c:116,524,662) does not change it. */
 #define DCTE_PLUGIN_EXACT 2u
 
 /* Build the map(s) for the frame handed to lqr_carver_new (src/render.c:312):
  * orientation 0 always, and the transposed frame's map too when
  * `with_transposed` (the plug-in passes vals->vertically, src/main.h:21:
- * liblqr transposes the carver for vertical resizes).  Returns DCTE_OK, or
- * an error code after which every lookup misses (the plug-in then runs its
- * original code). */
+ * liblqr transposes the carver for vertical resizes) -- both from one upload
+ * of the frame (dcte_energy_map2, or dcte_carver_create2 with the seam hook).
+ * Returns DCTE_OK, or an error code after which every lookup misses (the
+ * plug-in then runs its original code).  The glue's calls on its process-wide
+ * context are serialised by a mutex; the context is created once
+ * (pthread_once) by whichever thread comes first. */
 int dcte_plugin_build(dcte_map_cache *c, const uint8_t *px, int w, int h, int bpp,
                       size_t rowstride, int blocksize, float edges, float textures,
                       int with_transposed);
@@ -114,6 +121,19 @@ int dcte_plugin_lookup_hook(dcte_map_cache *c, int x, int y, int w, int h, int o
  * Exposed for tests. */
 int dcte_plugin_window_check(dcte_map_cache *c, int x, int y, int w, int h,
                              dcte_rwindow_read_fn rd, void *rw);
+
+/* The dialog preview (dct_energy_preview, src/render.c:421-501, called from
+ * src/interface.c:524): region = the preview rectangle's pixels as
+ * gimp_pixel_rgn_get_rect returns them (h rows of w * channels bytes,
+ * channels 1, 3 or 4 -- alpha ignored, as convert_row_to_luminance does,
+ * src/render.c:62-79); out = the drawn layer, w * h * channels bytes:
+ * normalize_image's DOUBLE2GUCHAR grey of dct_energy_preview_rows' energies
+ * (src/render.c:31-60, 80-109) in every channel.  flags: DCTE_PLUGIN_EXACT =
+ * the reference's bytes exactly; else the energies within 1e-5 relative (the
+ * bytes within +-1).  Returns DCTE_OK, or an error code (no device, channels
+ * 2) after which the plug-in runs its original loop. */
+int dcte_plugin_preview_u8(const uint8_t *region, int w, int h, int channels, int blocksize,
+                           float edges, float textures, unsigned flags, uint8_t *out);
 
 void dcte_plugin_release(dcte_map_cache *c);
 

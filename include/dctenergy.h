@@ -43,7 +43,12 @@
 extern "C" {
 #endif
 
-#define DCTE_ABI_VERSION 1
+/* ABI history.  1: first release.  2 (r06): DCTE_OPT_FAIL_INJECT moved from
+ * option id 8 to 9 (8 = the removed WIDE_BANDS, accepted as a no-op) -- a
+ * caller built against version 1 that arms id 8 injects nothing; new entry
+ * points dcte_energy_map2 and dcte_carver_create2; a dcte_carver keeps the
+ * arithmetic mode (DCTE_OPT_EXACT, DCTE_OPT_TIE_TAU) it was created in. */
+#define DCTE_ABI_VERSION 2
 
 /* status codes */
 #define DCTE_OK 0
@@ -102,7 +107,9 @@ extern "C" {
 #define DCTE_OPT_FAIL_INJECT 9 /* testing the error paths: 1 = the next map
                                launch is reported as failed (DCTE_EHIP) right
                                after it was queued; 2 = the next refinement
-                               launch likewise.  One-shot; 0 = off. */
+                               launch likewise (an exact-mode map call, which
+                               has no refinement launch, disarms it).
+                               One-shot; 0 = off.  (Id 8 in ABI version 1.) */
 #define DCTE_OPT_EXACT 10   /* 1 = bit-identical to the reference for every
                                pixel: the map is computed in the reference's
                                own fp64 operation order (ddct8x8s / ddct16x16s /
@@ -152,6 +159,21 @@ int dcte_set_option(dcte_ctx *ctx, int option, double value);
 int dcte_energy_map(dcte_ctx *ctx, const uint8_t *px, int w, int h, int bpp,
                     size_t rowstride, int n, float edges, float textures,
                     int semantics, int transposed, float *out);
+
+/* Both orientations of one frame from ONE upload (the plug-in's build for a
+ * vertical resize, src/render.c:358-364 with vals->vertically, src/main.h:21:
+ * liblqr transposes the carver, so its callbacks ask for the transposed
+ * frame's map, and the plug-in keeps the untransposed map too).  out (w*h
+ * floats, h rows of w) = dcte_energy_map(..., transposed = 0, out); out_t
+ * (w rows of h) = dcte_energy_map(..., transposed = 1, out_t): the same bits
+ * as the two calls.  Either may be NULL (not both).  One device: the frame is
+ * uploaded in row chunks with each chunk mapped and its map downloaded as it
+ * lands; the resident frame is then transposed in HBM and the transposed
+ * map computed and downloaded chunk by chunk.  Several devices: the two
+ * calls. */
+int dcte_energy_map2(dcte_ctx *ctx, const uint8_t *px, int w, int h, int bpp,
+                     size_t rowstride, int n, float edges, float textures,
+                     int semantics, float *out, float *out_t);
 
 /* Device-resident entry point (frames already in HBM; no copies, no sync).
  *   device    index into the context's devices
@@ -292,11 +314,23 @@ int dcte_carve(dcte_ctx *ctx, const uint8_t *px, int w, int h, int bpp, size_t r
  *   floats of the mirrored frame).
  * dcte_carver_step: one seam.  seam (height ints, columns in the frame before
  *   the step), band_x0 (height ints), band_e (height x band_width floats),
- *   band_px (height x band_width x bpp bytes): each optional. */
+ *   band_px (height x band_width x bpp bytes): each optional.
+ * Mode: a carver computes in the arithmetic the context was set to when the
+ *   carver was created (DCTE_OPT_EXACT, DCTE_OPT_TIE_TAU) for its whole life:
+ *   setting the context's options afterwards (another carver, a preview)
+ *   changes nothing for it.  (The reference's callback is bit-identical per
+ *   carver by construction, src/render.c:296-315.)
+ * dcte_carver_create2: also map_other_out (optional, w*h floats): the map of
+ *   the OTHER orientation of the same frame (transposed = 1: the frame as
+ *   given, h rows of w; transposed = 0: the transposed frame, w rows of h)
+ *   from the same upload -- the plug-in's vertical build needs both. */
 typedef struct dcte_carver dcte_carver;
 int dcte_carver_create(dcte_ctx *ctx, const uint8_t *px, int w, int h, int bpp, size_t rowstride,
                        int n, float edges, float textures, int transposed, float *map_out,
                        dcte_carver **out);
+int dcte_carver_create2(dcte_ctx *ctx, const uint8_t *px, int w, int h, int bpp, size_t rowstride,
+                        int n, float edges, float textures, int transposed, float *map_out,
+                        float *map_other_out, dcte_carver **out);
 int dcte_carver_step(dcte_carver *c, int *seam, int *band_x0, float *band_e, uint8_t *band_px);
 int dcte_carver_width(const dcte_carver *c);       /* current width of the mirrored frame */
 int dcte_carver_height(const dcte_carver *c);

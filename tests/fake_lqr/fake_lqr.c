@@ -385,11 +385,12 @@ int fake_window_check_selftest(int n, int bpp, unsigned seed)
  * The plug-in is built on px as in init_carver_from_vals; `hook` selects the
  * patched callback with the seam hook (DCTE_PLUGIN_SEAM_HOOK).  Outputs: the
  * final energies (fh x cw), the final image bytes (fh x cw x bpp), the seams
- * (seams x fh) and counts[11] = {callbacks, fallback (original transform),
+ * (seams x fh) and counts[12] = {callbacks, fallback (original transform),
  * served from a map, served from a seam band, mirror steps, nanoseconds spent
  * in the update_emap callbacks (incl. the mirror's steps), hook-served values
  * re-checked against the original body (verify), of those off tolerance,
- * hook misses, hook still on at the end, window reads of the hook's check}.
+ * hook misses, hook still on at the end, window reads of the hook's check,
+ * glue calls of the interleaved dialog that succeeded (fake_set_interleave)}.
  * transposed: vertical resize -- the carver works on the transposed frame.
  * diverge (tests of the hook's window check): 0 = liblqr follows the
  * mirror's rules; 1 = after the build liblqr's image differs slightly from
@@ -404,6 +405,76 @@ int fake_window_check_selftest(int n, int bpp, unsigned seed)
 /* extra plug-in build flags for fake_resize (DCTE_PLUGIN_EXACT) */
 static unsigned g_extra_flags;
 void fake_set_plugin_flags(unsigned flags) { g_extra_flags = flags; }
+
+/* The interactive dialog between the steps of a resize (src/interface.c:116,
+ * 524, 662): the preview redraws and another carver is set up, each in the
+ * DEFAULT (fast) mode, while the resize's own carver lives on.  With
+ * fake_set_interleave(1), fake_resize does this after its build and after
+ * every seam's update pass; the resize's energies must not change. */
+static int g_interleave;
+static long long g_interleaved;
+void fake_set_interleave(int on) { g_interleave = on; }
+
+static void dialog_interleave(const uint8_t *px, int w, int h, int bpp, int n, float edges,
+                              float textures)
+{
+    dcte_map_cache other;
+    if (dcte_plugin_build_ex(&other, px, w, h, bpp, (size_t)w * bpp, n, edges, textures, 1, 0u) ==
+        DCTE_OK)
+        g_interleaved++;
+    dcte_plugin_release(&other);
+    uint8_t *layer = (uint8_t *)malloc((size_t)w * h * bpp);
+    if (layer && dcte_plugin_preview_u8(px, w, h, bpp, n, edges, textures, 0u, layer) == DCTE_OK)
+        g_interleaved++;
+    free(layer);
+}
+
+/* The PATCHED dct_energy_preview on a drawable of
+ * dw x dh pixels with `channels` bytes each: the preview rectangle (x1, y1,
+ * w, h) is read as gimp_pixel_rgn_get_rect hands it over (copied out of the
+ * drawable, rows of w * channels bytes) and the glue draws the layer
+ * (dcte_plugin_preview_u8); when the glue fails (no device) the original loop
+ * runs -- dct_energy_preview_rows over the region (src/render.c:31-60, the
+ * oracle plays it) and normalize_image (src/render.c:80-109, DOUBLE2GUCHAR
+ * with GIMP's ROUND, src/render.h:6).  out: w * h * channels bytes.
+ * *gpu_status = the glue's return code. */
+int orc_preview_map_rows(const uint8_t *px, int w, int h, int bpp, size_t rowstride, int n,
+                         float edges, float textures, int y0, int y1, int nthreads, float *out); /* oracle */
+
+int fake_preview(const uint8_t *drawable, int dw, int dh, int channels, int x1, int y1, int w, int h,
+                 int n, float edges, float textures, unsigned flags, uint8_t *out, int *gpu_status)
+{
+    if (x1 < 0 || y1 < 0 || w <= 0 || h <= 0 || x1 + w > dw || y1 + h > dh) return -1;
+    uint8_t *region = (uint8_t *)malloc((size_t)w * h * channels);
+    if (!region) return -3;
+    for (int y = 0; y < h; y++)
+        memcpy(region + (size_t)y * w * channels,
+               drawable + ((size_t)(y1 + y) * dw + x1) * channels, (size_t)w * channels);
+    *gpu_status = dcte_plugin_preview_u8(region, w, h, channels, n, edges, textures, flags, out);
+    int rc = 0;
+    if (*gpu_status != DCTE_OK) {
+        float *E = (float *)malloc(sizeof(float) * (size_t)w * h);
+        if (!E || orc_preview_map_rows(region, w, h, channels, (size_t)w * channels, n, edges,
+                                       textures, 0, h, 1, E) != 0) {
+            rc = -2;
+        } else {
+            double mn = E[0], mx = E[0];
+            for (size_t i = 0; i < (size_t)w * h; i++) {
+                if (E[i] > mx) mx = E[i];
+                if (E[i] < mn) mn = E[i];
+            }
+            for (size_t i = 0; i < (size_t)w * h; i++) {
+                /* (the reference divides by zero on a flat region; the guard
+                 * draws 0 as the library does) */
+                const uint8_t v = mx > mn ? (uint8_t)(int)(255 * (((double)E[i] - mn) / (mx - mn)) + 0.5) : 0;
+                memset(out + i * channels, v, channels);
+            }
+        }
+        free(E);
+    }
+    free(region);
+    return rc;
+}
 
 int fake_resize(const uint8_t *px, int w, int h, int bpp, int n, float edges, float textures,
                 int use_gpu, int hook, int seams, int transposed, int diverge, int verify,
@@ -429,10 +500,11 @@ int fake_resize(const uint8_t *px, int w, int h, int bpp, int n, float edges, fl
     *gpu_status = use_gpu ? dcte_plugin_build_ex(&p.gpu, px, w, h, bpp, (size_t)w * bpp, n, edges,
                                                  textures, transposed, (hook ? DCTE_PLUGIN_SEAM_HOOK : 0u) | g_extra_flags)
                           : DCTE_ENODEV;
-    g_fallback_calls = g_served_map = g_verified = g_bad = 0;
+    g_fallback_calls = g_served_map = g_verified = g_bad = g_interleaved = 0;
     g_orientation = transposed;
     g_use_hook = hook;
     g_verify = verify;
+    if (g_interleave) dialog_interleave(px, w, h, bpp, n, edges, textures);
     long long calls = 0, update_ns = 0;
     int cw = fw;
     const int r = n / 2;
@@ -487,6 +559,7 @@ int fake_resize(const uint8_t *px, int w, int h, int bpp, int n, float edges, fl
             }
         clock_gettime(CLOCK_MONOTONIC, &t1);
         update_ns += (t1.tv_sec - t0.tv_sec) * 1000000000LL + (t1.tv_nsec - t0.tv_nsec);
+        if (g_interleave) dialog_interleave(px, w, h, bpp, n, edges, textures);
         if (diverge == 4 && k == 0) {
             for (size_t i = 0; i < (size_t)cw * fh; i++) luma[i] += 1e-3 * (double)(i % 7) / 7.0;
             for (int y = 0; y < fh; y++)
@@ -511,6 +584,7 @@ int fake_resize(const uint8_t *px, int w, int h, int bpp, int n, float edges, fl
     counts[8] = p.gpu.missed;
     counts[9] = p.gpu.hook_ok;
     counts[10] = p.gpu.reads;
+    counts[11] = g_interleaved;
     dcte_plugin_release(&p.gpu);
     g_use_hook = g_verify = 0;
     free(img);

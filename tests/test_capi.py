@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_strerror():
     L = dctenergy.lib()
-    assert L.dcte_abi_version() == 1
+    assert L.dcte_abi_version() == 2
     for code in (0, -1, -2, -3, -4, -5, -6):
         assert L.dcte_strerror(code)
     assert L.dcte_strerror(-99) == b"unknown error"

@@ -525,6 +525,64 @@ def test_transposed_map(ctx, n):
         _assert_tol(got, O.energy_map(tr, n, 0.15, 0.85), name)
 
 
+@pytest.mark.parametrize("n", [2, 4, 8, 16])
+def test_energy_map2_is_the_two_calls(ctx, n):
+    """dcte_energy_map2 (the plug-in's vertical build,
+    src/render.c:358-364): both orientations from one upload, bit-equal to
+    the two dcte_energy_map calls -- every semantics, ragged and tall frames
+    (several row chunks each way), either output alone."""
+    rng = np.random.default_rng(n)
+    tall = rng.integers(0, 256, (3001, 700, 3), dtype=np.uint8)
+    tall[:, 200:420] //= 9                        # flat stretch: ties, refinement
+    for img in (load_input("natural_rgb_73x59.npy"), load_input("natural_grey_200x120.npy"),
+                load_input("tiny_rgb_5x1.npy"), tall):
+        for sem in (dctenergy.DCTE_LQR, dctenergy.DCTE_PREVIEW):
+            a = ctx.energy_map(img, n, 0.3, 0.7, semantics=sem)
+            b = ctx.energy_map(img, n, 0.3, 0.7, semantics=sem, transposed=True)
+            o, ot = ctx.energy_map2(img, n, 0.3, 0.7, semantics=sem)
+            assert np.array_equal(o, a) and np.array_equal(ot, b), (img.shape, sem)
+            o1, none = ctx.energy_map2(img, n, 0.3, 0.7, semantics=sem, want=(True, False))
+            none2, ot1 = ctx.energy_map2(img, n, 0.3, 0.7, semantics=sem, want=(False, True))
+            assert none is None and none2 is None
+            assert np.array_equal(o1, a) and np.array_equal(ot1, b), (img.shape, sem)
+        if img is not tall:
+            tr = np.ascontiguousarray(np.swapaxes(img, 0, 1))
+            _assert_tol(ot, O.preview_map(tr, n, 0.3, 0.7), img.shape)
+
+
+def test_energy_map2_exact_and_multi_device(ctx):
+    """The exact mode through dcte_energy_map2 is the reference's bits in both
+    orientations; on G logical devices (the row-band host path) the same maps
+    as on one."""
+    img = load_input("wilber_rgb_74x59.npy")
+    tr = np.ascontiguousarray(np.swapaxes(img, 0, 1))
+    with dctenergy.Context(ngpus=1, exact=True) as ex:
+        for n in (2, 4, 8, 16):
+            o, ot = ex.energy_map2(img, n, 0.3, 0.7)
+            assert np.array_equal(o, O.energy_map(img, n, 0.3, 0.7)), n
+            assert np.array_equal(ot, O.energy_map(tr, n, 0.3, 0.7)), n
+    big = np.random.default_rng(5).integers(0, 256, (1500, 333, 3), dtype=np.uint8)
+    with dctenergy.Context(ngpus=3, same_device=True) as many:
+        for n in (8, 16):
+            o, ot = ctx.energy_map2(big, n, 0.3, 0.7)
+            o3, ot3 = many.energy_map2(big, n, 0.3, 0.7)
+            assert np.array_equal(o, o3) and np.array_equal(ot, ot3), n
+
+
+@pytest.mark.parametrize("transposed", [False, True])
+def test_carver_create2_other_orientation(ctx, transposed):
+    """dcte_carver_create2: the mirror's first map and the OTHER orientation's
+    map from the same upload == dcte_energy_map of each orientation."""
+    img = load_input("natural_rgb_97x41.npy")
+    for n in (4, 8, 16):
+        c, first, second = ctx.carver(img, n, 0.3, 0.7, transposed, other=True)
+        a = ctx.energy_map(img, n, 0.3, 0.7)
+        b = ctx.energy_map(img, n, 0.3, 0.7, transposed=True)
+        assert np.array_equal(first, b if transposed else a), n
+        assert np.array_equal(second, a if transposed else b), n
+        c.close()
+
+
 def test_sharded_energy_image_u8_single_rank(ctx):
     """dist.energy_image_u8 (band min/max -> all-reduce -> normalise) on one
     rank equals the fused host entry point; the multi-rank reduction and the

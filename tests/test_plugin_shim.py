@@ -16,7 +16,7 @@ import pytest
 
 import dctenergy
 import oracle_py as O
-from golden_util import load_input, within_tol
+from golden_util import load_input, load_map, manifest, within_tol
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 FAKE_DIR = os.path.join(HERE, "fake_lqr")
@@ -44,6 +44,13 @@ def fake():
                                   ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_int)]
         L.fake_set_plugin_flags.restype = None
         L.fake_set_plugin_flags.argtypes = [ctypes.c_uint]
+        L.fake_set_interleave.restype = None
+        L.fake_set_interleave.argtypes = [ctypes.c_int]
+        L.fake_preview.restype = ctypes.c_int
+        L.fake_preview.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_uint,
+                                   ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
         L.fake_window_check_selftest.restype = ctypes.c_int
         L.fake_window_check_selftest.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint]
         _lib = L
@@ -79,7 +86,7 @@ def resize(img, n, e, t, seams, use_gpu, hook, transposed=False, diverge="none",
     emap = np.empty((fh, fw - seams), np.float32)
     px = np.empty((fh, fw - seams) + img.shape[2:], np.uint8)
     seam_cols = np.empty((max(seams, 1), fh), np.int32)
-    counts = (ctypes.c_longlong * 11)()
+    counts = (ctypes.c_longlong * 12)()
     status = ctypes.c_int()
     rc = fake().fake_resize(img.ctypes.data, w, h, bpp, n, e, t, int(use_gpu), int(hook), seams,
                             int(transposed), DIVERGE[diverge], int(verify), emap.ctypes.data,
@@ -89,7 +96,23 @@ def resize(img, n, e, t, seams, use_gpu, hook, transposed=False, diverge="none",
     return {"emap": emap, "px": px, "seams": seam_cols[:seams], "callbacks": c[0],
             "fallback": c[1], "served_map": c[2], "served_band": c[3], "steps": c[4], "update_ns": c[5],
             "verified": c[6], "bad": c[7], "missed": c[8], "hook_on": c[9], "reads": c[10],
-            "status": status.value, "initial": fw * fh}
+            "interleaved": c[11], "status": status.value, "initial": fw * fh}
+
+
+def preview(drawable, n, e, t, flags=0, rect=None):
+    """The patched dct_energy_preview of tests/fake_lqr
+    on an HxW(xC) drawable; rect = (x1, y1, w, h), default the whole
+    drawable -> (drawn u8 layer h x w (x C), the glue's status)."""
+    d = np.ascontiguousarray(drawable)
+    dh, dw = d.shape[:2]
+    ch = 1 if d.ndim == 2 else d.shape[2]
+    x1, y1, w, h = rect or (0, 0, dw, dh)
+    out = np.empty((h, w) + ((ch,) if ch > 1 else ()), np.uint8)
+    status = ctypes.c_int()
+    rc = fake().fake_preview(d.ctypes.data, dw, dh, ch, x1, y1, w, h, n, e, t, flags,
+                             out.ctypes.data, ctypes.byref(status))
+    assert rc == 0
+    return out, status.value
 
 
 @pytest.mark.parametrize("n", [2, 4, 8, 16])
@@ -298,3 +321,127 @@ def test_exact_plugin_resize_is_the_reference(n, transposed):
         assert np.array_equal(d["seams"][k], ref_seam), f"seam {k}"
         host = np.stack([np.delete(host[y], ref_seam[y], axis=0) for y in range(host.shape[0])])
     assert np.array_equal(d["emap"], O.energy_map(d["px"], n, 0.3, 0.7))
+
+
+def _reference_resize(img, n, e, t, seams, transposed):
+    """The CPU reference loop: per seam the oracle's map, its seam, the carve."""
+    host = np.ascontiguousarray(np.swapaxes(img, 0, 1)) if transposed else img
+    out = []
+    for _ in range(seams):
+        s = O.seam_find(O.energy_map(host, n, e, t))
+        out.append(s)
+        host = np.stack([np.delete(host[y], s[y], axis=0) for y in range(host.shape[0])])
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,transposed", [(8, False), (16, False), (4, True)])
+def test_exact_carver_keeps_its_mode_through_fast_dialog_calls(n, transposed):
+    """The mode belongs to the carver: an exact carver
+    built first, then -- after its build and after every seam -- the dialog
+    redraws the preview and sets up another carver in the fast mode on the
+    same shared context.  The exact carver's resize loop still cuts the CPU
+    reference loop's seams and ends with exactly the reference map of its
+    image."""
+    img = load_input("wilber_rgb_74x59.npy")
+    fake().fake_set_plugin_flags(2)               # DCTE_PLUGIN_EXACT
+    fake().fake_set_interleave(1)
+    try:
+        d = resize(img, n, 0.3, 0.7, 8, use_gpu=True, hook=True, transposed=transposed)
+    finally:
+        fake().fake_set_plugin_flags(0)
+        fake().fake_set_interleave(0)
+    assert d["status"] == dctenergy.DCTE_OK
+    assert d["interleaved"] == 2 * (8 + 1)       # a fast build and a fast preview each time
+    assert d["steps"] == 8 and d["hook_on"] == 1 and d["fallback"] == 0
+    for k, ref_seam in enumerate(_reference_resize(img, n, 0.3, 0.7, 8, transposed)):
+        assert np.array_equal(d["seams"][k], ref_seam), f"seam {k}"
+    assert np.array_equal(d["emap"], O.energy_map(d["px"], n, 0.3, 0.7))
+
+
+@pytest.mark.gpu
+def test_carver_mode_is_captured_at_create():
+    """ABI level: a dcte_carver created in the exact mode keeps computing its
+    band energies in it after the context is switched to the fast mode (and
+    a fast carver stays fast after the context is switched to exact)."""
+    img = load_input("wilber_rgb_74x59.npy")
+    with dctenergy.Context(ngpus=1, exact=True) as ctx:
+        c, first = ctx.carver(img, 8, 0.3, 0.7)
+        ctx.set_option(dctenergy.DCTE_OPT_EXACT, 0)
+        fast_map = ctx.energy_map(img, 8, 0.3, 0.7)     # a fast call in between
+        assert np.array_equal(first, O.energy_map(img, 8, 0.3, 0.7))
+        px = img.copy()
+        for _ in range(5):
+            seam, x0, e, bpx = c.step()
+            px = np.ascontiguousarray(np.stack([np.delete(px[y], seam[y], axis=0)
+                                                for y in range(px.shape[0])]))
+            ref = O.energy_map(px, 8, 0.3, 0.7)
+            W = px.shape[1]
+            for y in range(px.shape[0]):
+                cols = np.minimum(x0[y] + np.arange(c.band_width), W - 1)
+                assert np.array_equal(e[y], ref[y, cols])
+        c.close()
+        assert within_tol(fast_map, O.energy_map(img, 8, 0.3, 0.7)).all()
+
+
+@pytest.mark.gpu
+def test_plugin_preview_is_the_golden_layer():
+    """dcte_plugin_preview_u8 through the patched dct_energy_preview: every
+    golden preview layer (tests/golden, from the reference's transforms) --
+    bit-identical with DCTE_PLUGIN_EXACT, within +-1 in the fast mode."""
+    entries = manifest()["preview"]
+    assert entries
+    for entry in entries:
+        img = load_input(entry["input"])
+        want = load_map(entry["output_u8"])
+        if entry["channels"] != (1 if img.ndim == 2 else img.shape[2]):
+            continue
+        got, st = preview(img, entry["N"], entry["edges"], entry["textures"], flags=2)
+        assert st == dctenergy.DCTE_OK
+        assert np.array_equal(got, want), entry["output_u8"]
+        got, st = preview(img, entry["N"], entry["edges"], entry["textures"], flags=0)
+        assert st == dctenergy.DCTE_OK
+        assert np.abs(got.astype(int) - want.astype(int)).max() <= 1, entry["output_u8"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 4, 8, 16])
+def test_plugin_preview_rectangle(n):
+    """A preview rectangle inside a larger drawable: the region-relative
+    clamp of src/render.c:456-468 (the rectangle's own rows and columns)."""
+    img = load_input("natural_rgb_97x41.npy")
+    rect = (13, 7, 61, 29)
+    x1, y1, w, h = rect
+    region = np.ascontiguousarray(img[y1:y1 + h, x1:x1 + w])
+    want = O.normalize_preview(O.preview_map(region, n, 0.3, 0.7), channels=3)
+    got, st = preview(img, n, 0.3, 0.7, flags=2, rect=rect)
+    assert st == dctenergy.DCTE_OK
+    assert np.array_equal(got, want)
+
+
+def test_plugin_preview_without_gpu():
+    """CPU: no device -> the glue reports it and the original loop draws the
+    layer: the golden preview layers exactly."""
+    if dctenergy.device_count() > 0:
+        pytest.skip("device visible; covered by the GPU test")
+    for entry in manifest()["preview"]:
+        img = load_input(entry["input"])
+        if entry["channels"] != (1 if img.ndim == 2 else img.shape[2]):
+            continue
+        got, st = preview(img, entry["N"], entry["edges"], entry["textures"], flags=2)
+        assert st == dctenergy.DCTE_ENODEV
+        assert np.array_equal(got, load_map(entry["output_u8"])), entry["output_u8"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [4, 8])
+def test_seam_hook_repass_on_one_row(n):
+    """A re-pass that starts on the previous callback's row: on a
+    1-row frame every pass is one row, so only the column order tells a new
+    pass; the hook must re-check and, liblqr's image having changed, switch
+    itself off without serving a foreign value."""
+    img = np.ascontiguousarray(load_input("natural_rgb_97x41.npy")[20:21])
+    d = resize(img, n, 0.3, 0.7, 4, use_gpu=True, hook=True, diverge="repass", verify=True)
+    assert d["status"] == dctenergy.DCTE_OK
+    assert d["bad"] == 0 and d["verified"] == d["served_band"]
+    assert d["hook_on"] == 0 and d["fallback"] > 0
