@@ -25,7 +25,14 @@
 
 namespace {
 
-constexpr double kDefaultTieTau = 4e-6;
+// Default refinement margins per N (DCTE_OPT_TIE_TAU unset): at least twice
+// the DERIVED worst-case relative error of m_e and m_t together against the
+// reference (fp32 rounding of the committed operation sequence, the fp32
+// constants, the reference's own fp64 and luma rounding) -- tests/emu/
+// tau_bound.cpp, asserted by tests/test_tau_bound.py, DESIGN.md §5:
+// N = 2: 0.49e-6, 4: 1.74e-6, 8: 7.9e-6, 16: 2.31e-5.  (r02-r05 used 4e-6 for
+// every N, set from an adversarial search; its worst find is 7.7e-7.)
+double default_tie_tau(int n) { return n == 16 ? 5e-5 : n == 8 ? 2e-5 : 4e-6; }
 constexpr int kMaxGridY = 65535;   // launch grid limit in y (map tiles of a band)
 constexpr int kCountWords = 8;     // FixScratch::d_count
 
@@ -113,7 +120,7 @@ struct ProfEvent {
 
 struct dcte_ctx {
     std::vector<Device> devs;
-    double tie_tau = kDefaultTieTau;
+    double tie_tau = -1;            // DCTE_OPT_TIE_TAU; < 0: default_tie_tau(N)
     bool profile = false;
     double pin_mib = 1.0;           // DCTE_OPT_PIN_HOST (64 before r05: 4096^2 2.44 -> 1.67 ms at 1)
     int tile_h = 0;                 // DCTE_OPT_TILE_H (0: the kernel's default)
@@ -157,7 +164,10 @@ bool valid_n(int n) { return n == 2 || n == 4 || n == 8 || n == 16; }
 // the refinement margin a call uses: the exact mode refines every pixel it
 // does not compute in fp64 outright (seam bands and points; every map call
 // goes to dcte_exact.hip's sliding kernels)
-double eff_tau(const dcte_ctx* ctx) { return ctx->exact ? 1.0 : ctx->tie_tau; }
+double eff_tau(const dcte_ctx* ctx, int n)
+{
+    return ctx->exact ? 1.0 : ctx->tie_tau >= 0 ? ctx->tie_tau : default_tie_tau(n);
+}
 
 // Runs a block of calls in a given arithmetic mode and restores the
 // context's own afterwards: a dcte_carver carries the mode it was created in
@@ -478,7 +488,7 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     p.out_stride = out_stride;
     p.we = (float)((double)edges / scale);
     p.wt = (float)((double)textures / scale);
-    p.tie_tau = (float)eff_tau(ctx);
+    p.tie_tau = (float)eff_tau(ctx, n);
     p.edges = edges;
     p.textures = textures;
     p.fix_list = f->d_list;
@@ -529,7 +539,7 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     };
     if (injected(1)) return fail(hipErrorLaunchFailure, "launch_map (injected)");
     f->phase ^= 1u;   // the launch ran: the next one uses the counter it zeroed
-    if ((p.we != p.wt && eff_tau(ctx) > 0) || eff_tau(ctx) >= 1.0) {
+    if ((p.we != p.wt && eff_tau(ctx, n) > 0) || eff_tau(ctx, n) >= 1.0) {
         if ((e = dcte::launch_fix_tiles(n, bpp, sem, q, s)) != hipSuccess) return fail(e, "launch_fix_tiles");
         if (injected(2)) return fail(hipErrorLaunchFailure, "launch_fix_tiles (injected)");
     }
@@ -902,8 +912,8 @@ int dcte_set_option(dcte_ctx* ctx, int option, double value)
     if (!ctx) return DCTE_EINVAL;
     switch (option) {
     case DCTE_OPT_TIE_TAU:
-        if (!(value >= 0)) return DCTE_EINVAL;
-        ctx->tie_tau = value;
+        if (value != value) return DCTE_EINVAL;
+        ctx->tie_tau = value < 0 ? -1 : value;   // < 0: the per-N defaults again
         return DCTE_OK;
     case DCTE_OPT_PROFILE:
         ctx->profile = value != 0;
@@ -1015,13 +1025,13 @@ int dcte_seam_carve_device(dcte_ctx* ctx, int device, const void* d_px, long lon
     p.map_out_stride = map_out_stride;
     p.we = (float)((double)edges / scale);
     p.wt = (float)((double)textures / scale);
-    p.tie_tau = (float)eff_tau(ctx);
+    p.tie_tau = (float)eff_tau(ctx, n);
     p.fix_count = f->d_count;
     p.fix_list = f->d_list;
     p.fix_cap = (unsigned)f->cap;
     DCTE_HIP(ctx, hipMemsetAsync(f->d_count, 0, sizeof(unsigned), s));
     DCTE_HIP(ctx, dcte::launch_seam_carve(p, s));
-    if ((p.we != p.wt && eff_tau(ctx) > 0) || eff_tau(ctx) >= 1.0) {
+    if ((p.we != p.wt && eff_tau(ctx, n) > 0) || eff_tau(ctx, n) >= 1.0) {
         dcte::FixParams q = fix_params(p.px_out, out_rowstride, w - 1, h, 0, bpp, n, 0, semantics,
                                        d_map_out, map_out_stride, edges, textures, f);
         DCTE_HIP(ctx, dcte::launch_fix(q, s));
@@ -1062,13 +1072,13 @@ int dcte_energy_points_device(dcte_ctx* ctx, int device, const void* d_px, long 
     p.map_out = d_out;
     p.we = (float)((double)edges / scale);
     p.wt = (float)((double)textures / scale);
-    p.tie_tau = (float)eff_tau(ctx);
+    p.tie_tau = (float)eff_tau(ctx, n);
     p.fix_count = f->d_count;
     p.fix_list = f->d_list;
     p.fix_cap = (unsigned)f->cap;
     DCTE_HIP(ctx, hipMemsetAsync(f->d_count, 0, sizeof(unsigned), s));
     DCTE_HIP(ctx, dcte::launch_points(p, s));
-    if ((p.we != p.wt && eff_tau(ctx) > 0) || eff_tau(ctx) >= 1.0) {
+    if ((p.we != p.wt && eff_tau(ctx, n) > 0) || eff_tau(ctx, n) >= 1.0) {
         dcte::FixParams q = fix_params(p.px, rowstride, w, h, 0, bpp, n, 0, semantics, d_out, 0,
                                        edges, textures, f);
         q.pts = d_xy;

@@ -73,8 +73,11 @@ extern "C" {
 
 /* options for dcte_set_option */
 #define DCTE_OPT_TIE_TAU 1 /* relative edge/texture margin refined in fp64
-                              (default 4e-6; 0 = never refine, >= 1 = refine
-                              every pixel) */
+                              (default per N: 4e-6 for N = 2, 4; 2e-5 for
+                              N = 8; 5e-5 for N = 16 -- at least twice the
+                              derived worst-case fp32 error, DESIGN.md §5;
+                              a negative value restores these defaults;
+                              0 = never refine, >= 1 = refine every pixel) */
 #define DCTE_OPT_PROFILE 2 /* 1 = bracket every map-kernel launch with HIP
                               events on its stream (dcte_profile_read) */
 #define DCTE_OPT_PIN_HOST 3 /* host entry points: page-lock the caller's frame

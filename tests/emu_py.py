@@ -9,7 +9,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 EMU_DIR = os.path.join(HERE, "emu")
 EMU_SO = os.path.join(EMU_DIR, "build", "libdcte_emu.so")
 LUMA_SCALE = 1275000.0
-TIE_TAU = 4e-6   # kDefaultTieTau in dcte_capi.cpp
+# default_tie_tau(N) in dcte_capi.cpp: twice the derived error bound (test_tau_bound.py)
+TIE_TAU = {2: 4e-6, 4: 4e-6, 8: 2e-5, 16: 5e-5}
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _f32p = ctypes.POINTER(ctypes.c_float)
@@ -83,8 +84,11 @@ def energy_map(img, n, edges, textures, sem=0):
     return E, me, mt
 
 
-def refine_mask(me, mt, edges, textures, tau=TIE_TAU):
-    """Pixels the kernel hands to the fp64 refinement (same predicate)."""
+def refine_mask(me, mt, edges, textures, n, tau=None):
+    """Pixels the kernel hands to the fp64 refinement (same predicate; tau
+    defaults to the library's margin for N)."""
+    if tau is None:
+        tau = TIE_TAU[n]
     if np.float32(edges) == np.float32(textures):
         return np.zeros(me.shape, bool)
     hi = np.maximum(me, mt)

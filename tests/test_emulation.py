@@ -20,7 +20,7 @@ def _check(img, n, e, t, ref=None):
     if ref is None:
         ref = O.energy_map(img, n, e, t)
     E, me, mt = EM.energy_map(img, n, e, t)
-    refine = EM.refine_mask(me, mt, e, t)
+    refine = EM.refine_mask(me, mt, e, t, n)
     ok = np.abs(E.astype(np.float64) - ref) <= RTOL * np.abs(ref.astype(np.float64)) + ATOL
     bad = ~ok & ~refine
     assert not bad.any(), (f"N={n}: {bad.sum()} unrefined pixels off tolerance, e.g. "
@@ -92,6 +92,6 @@ def test_emulated_kernel_vs_golden_preview(entry):
     img = load_input(entry["input"])
     ref = load_map(entry["output"])
     E, me, mt = EM.energy_map(img, entry["N"], entry["edges"], entry["textures"], sem=1)
-    refine = EM.refine_mask(me, mt, entry["edges"], entry["textures"])
+    refine = EM.refine_mask(me, mt, entry["edges"], entry["textures"], entry["N"])
     ok = np.abs(E.astype(np.float64) - ref) <= RTOL * np.abs(ref.astype(np.float64)) + ATOL
     assert not (~ok & ~refine).any()

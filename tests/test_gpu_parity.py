@@ -411,7 +411,7 @@ def test_ties_are_refined_to_reference(ctx):
             # the device flags exactly the pixels the emulated fp32 path puts
             # inside the refinement band
             _, me, mt = EM.energy_map(img, n, 0.3, 0.7)
-            assert ctx.last_refined == int(EM.refine_mask(me, mt, 0.3, 0.7).sum())
+            assert ctx.last_refined == int(EM.refine_mask(me, mt, 0.3, 0.7, n).sum())
             if n < 16:
                 assert ctx.last_refined > 0
 

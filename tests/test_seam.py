@@ -90,7 +90,7 @@ def test_carve_refine_all_is_reference_exact(ctx, n):
     try:
         host, E = _carve_run(ctx, img, n, 0.15, 0.85, 0, _seams(3, 6))
     finally:
-        ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, 4e-6)
+        ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, -1)   # the per-N defaults
     assert np.array_equal(E, O.energy_map(host, n, 0.15, 0.85))
 
 

@@ -163,7 +163,7 @@ def test_carve_loop_refined_equals_cpu_reference_loop(ctx, n):
     try:
         seams, _, frame, E = _gpu_loop(ctx, img, n, 0.3, 0.7, 10)
     finally:
-        ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, 4e-6)
+        ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, -1)   # the per-N defaults
     host = img
     for k in range(10):
         ref_seam = O.seam_find(O.energy_map(host, n, 0.3, 0.7))
@@ -196,7 +196,7 @@ def test_host_carve_refined_equals_cpu_reference_loop(ctx, n):
     try:
         out, cols = ctx.carve(img, 10, n, 0.3, 0.7)
     finally:
-        ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, 4e-6)
+        ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, -1)   # the per-N defaults
     host = img
     for k in range(10):
         ref_seam = O.seam_find(O.energy_map(host, n, 0.3, 0.7))
