@@ -235,6 +235,60 @@ def host_path(ctx, frame_dev, n, e, t, iters=3):
                     f"H2D and the map's D2H at once on two streams from pinned buffers"}
 
 
+def host_path_vertical(ctx, frame_dev, n, e, t, iters=3):
+    """The plug-in's build for a VERTICAL resize (vals->vertically,
+    src/render.c:358-364, src/main.h:21): both orientations' maps of the
+    pageable host frame -- dcte_energy_map2, one upload, the transposed map
+    chunked so its download overlaps the launches.  Floor = the frame's H2D
+    and the two maps' D2H at once on two streams from pinned buffers."""
+    import numpy as np
+    import torch
+    px = frame_dev.cpu().numpy()
+    H, W = px.shape[:2]
+    out = np.empty((H, W), np.float32)
+    out_t = np.empty((W, H), np.float32)
+    ctx.energy_map2(px, n, e, t, out=out, out_t=out_t)
+    ts = []
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        ctx.energy_map2(px, n, e, t, out=out, out_t=out_t)
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    med = ts[len(ts) // 2]
+    # the two separate calls the glue made before (r05), for comparison
+    t0 = time.perf_counter()
+    ctx.energy_map(px, n, e, t, out=out)
+    ctx.energy_map(px, n, e, t, transposed=True, out=out_t)
+    two_calls = time.perf_counter() - t0
+    px_pin = torch.empty(tuple(px.shape), dtype=torch.uint8, pin_memory=True)
+    out_pin = torch.empty((H, W), dtype=torch.float32, pin_memory=True)
+    out_pin2 = torch.empty((W, H), dtype=torch.float32, pin_memory=True)
+    d_px = torch.empty(tuple(px.shape), dtype=torch.uint8, device=frame_dev.device)
+    d_out = torch.empty((H, W), dtype=torch.float32, device=frame_dev.device)
+    s_up, s_down = torch.cuda.Stream(frame_dev.device), torch.cuda.Stream(frame_dev.device)
+    fl = []
+    for _ in range(iters + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(s_up):
+            d_px.copy_(px_pin, non_blocking=True)
+        with torch.cuda.stream(s_down):
+            out_pin.copy_(d_out, non_blocking=True)
+            out_pin2.view(H, W).copy_(d_out, non_blocking=True)
+        torch.cuda.synchronize()
+        fl.append(time.perf_counter() - t0)
+    floor = sorted(fl[1:])[len(fl[1:]) // 2]
+    del px_pin, out_pin, out_pin2, d_px, d_out
+    return {"value": round(H * W / med / 1e9, 2), "unit": "Gpx/s (frame pixels, both maps)",
+            "ms": round(med * 1e3, 2), "best_ms": round(ts[0] * 1e3, 2), "iters": iters,
+            "two_calls_ms": round(two_calls * 1e3, 2),
+            "bytes_h2d": int(px.nbytes), "bytes_d2h": int(2 * out.nbytes),
+            "duplex_floor_ms": round(floor * 1e3, 2), "ratio_to_floor": round(med / floor, 3),
+            "what": f"{H}x{W} RGB pageable host frame -> dcte_energy_map2 -> both maps on the host "
+                    f"(one upload; PCIe-inclusive); floor = one H2D and two D2H at once on two "
+                    f"streams from pinned buffers; two_calls = the r05 glue's two dcte_energy_map calls"}
+
+
 def stress(ctx, n, S, e, t, dev, stream, iters=10, rounds=3):
     """The worst realistic frame for the fp64 tie refinement, timed like the
     headline after it: line-art RGB (black lines on white every 23 rows, every
@@ -335,6 +389,8 @@ def other_configs(ctx, e, t, dev, stream, iters=20, rounds=3):
                     "value": round(S * S / best_call / 1e3, 1), "unit": "Mpx/s",
                     "hbm_frac_of_map": round(S * S * 7 / (best_map * 1e-3) / 8.0e12, 4)}
         del fr, out
+        if n == 16:                    # the N = 16 tie-dense worst case beside it
+            res[key]["stress"] = stress(ctx, 16, S, e, t, dev, stream)
     torch.cuda.empty_cache()
     res["what"] = ("BASELINE configs[1] and configs[4] after the timed region (the headline is "
                    "configs[2]); call = map + tie refinement, as the headline's step")
@@ -761,8 +817,15 @@ def main():
             res["stress"] = stress(ctx, n, S, e, t, dev, stream)
         if world == 1 and not args.no_exact:
             res["exact"] = exact(n, S, e, t, dev, buf)
+        if world == 1 and not args.no_configs and S == 16384 and n == 8:
+            res["configs_1gpu"] = other_configs(ctx, e, t, dev, stream)
+        # (r05 timed the host path before configs_1gpu: after other device
+        # work its SDMA download and upload were serialised by the runtime, 38
+        # instead of 22.4 ms; since r06 the download is a copy kernel, and
+        # the order no longer matters -- tools/host_diag.py)
         if world == 1 and not args.no_host_path:
             res["host_path"] = host_path(ctx, buf, n, e, t)
+            res["host_path_vertical"] = host_path_vertical(ctx, buf, n, e, t)
             if S > 4096:                       # BASELINE configs[1]'s frame size, a 4096^2 crop
                 res["host_path_4096"] = host_path(ctx, buf[:4096, :4096].contiguous(), n, e, t, iters=7)
         if world == 1 and not args.no_cpu_baseline:
@@ -770,12 +833,6 @@ def main():
             rows = min(rows, H)
             host = buf[:min(H, rows + n)].cpu().numpy()
             res["cpu_baseline"] = cpu_baseline(host, W, n, e, t, rows)
-        # last: after its synthetic frames are generated and freed on the
-        # device, the page-locked host path of this process ran at 38 instead
-        # of 22.4 ms (torch's own pinned copies and a registered buffer's bare
-        # copy did not change; tools/_diag_host.py) -- so it goes after host_path
-        if world == 1 and not args.no_configs and S == 16384 and n == 8:
-            res["configs_1gpu"] = other_configs(ctx, e, t, dev, stream)
         print(json.dumps(res), file=result_out, flush=True)
     ctx.close()
     if world > 1:

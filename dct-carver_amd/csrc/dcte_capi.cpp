@@ -8,6 +8,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <new>
 #include <mutex>
@@ -129,6 +130,7 @@ struct dcte_ctx {
     unsigned long long* stamps = nullptr;   // DCTE_OPT_TSTAMP_BUF (timing-probe builds)
     int fail_inject = 0;            // DCTE_OPT_FAIL_INJECT (tests of the error paths)
     bool exact = false;             // DCTE_OPT_EXACT
+    bool d2h_kernel = true;         // DCTE_OPT_D2H_KERNEL
     std::vector<ProfEvent> prof;
     long long last_refined = 0;
     std::string last_error;
@@ -576,18 +578,53 @@ bool valid_norm(int mode, int channels)
 // Page-locks a caller buffer for the duration of a host call (RAII).  A
 // buffer that is already pinned, or that the runtime refuses, stays as it is:
 // pinning only lets the chunk copies overlap, it never changes results.
-// The range registered is exactly the caller's bytes: a page-rounded range
-// makes the runtime reject (invalid argument) a copy to a neighbouring buffer
-// that shares the first or last page -- the output array numpy allocates
-// right after the frame, say (tools/pin_probe.cpp, profiles/r05/pin_probe.txt).
+// Only the WHOLE pages inside the caller's bytes are registered, [lo, hi):
+// a page the buffer shares with a neighbour is never locked by us.  (r05
+// registered exactly the caller's bytes, after a page-rounded range had made
+// the runtime refuse copies into a neighbour -- tools/pin_probe.cpp; but the
+// runtime locks whole pages, and a pageable copy of a neighbour sharing the
+// first or last page -- the runtime pins such copies on the fly and unpins
+// them afterwards -- then left the download into our buffer faulting
+// (hipErrorIllegalAddress at the sync: test_extreme_aspect_ratios, a
+// 3 x 100003 grey frame whose 300 KB frame copy is pageable and whose 1.2 MB
+// map is registered).)  The copies split at lo and hi: the partial pages at
+// either end go through the runtime's pageable path (upload_rows, download).
+// With `mapped`, also the device address of lo (dev) for a copy kernel to
+// write into; a caller-pinned buffer (hipHostMalloc, or registered by the
+// caller) is used whole, with its own device address.
 struct HostPin {
-    void* base = nullptr;
-    HostPin(const dcte_ctx* ctx, const void* p, size_t bytes)
+    void* base = nullptr;            // what we registered (unregistered at the end)
+    uintptr_t lo = 0, hi = 0;        // pinned host range
+    void* dev = nullptr;             // device address of lo (mapped), or null
+    HostPin(const dcte_ctx* ctx, const void* p, size_t bytes, bool mapped = false)
     {
-        if (ctx->pin_mib <= 0 || (double)bytes < ctx->pin_mib * 1048576.0) return;
+        if (!p || ctx->pin_mib <= 0 || (double)bytes < ctx->pin_mib * 1048576.0) return;
+        const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + 4095u) & ~(uintptr_t)4095u;
+        const uintptr_t b = (reinterpret_cast<uintptr_t>(p) + bytes) & ~(uintptr_t)4095u;
         void* v = const_cast<void*>(p);
-        if (hipHostRegister(v, bytes, hipHostRegisterDefault) == hipSuccess) base = v;
-        else (void)hipGetLastError();
+        // a caller-pinned buffer first (registering part of it would fail)
+        void* cdev = nullptr;
+        if (hipHostGetDevicePointer(&cdev, v, 0) == hipSuccess && cdev) {
+            lo = reinterpret_cast<uintptr_t>(p);
+            hi = lo + bytes;
+            dev = mapped ? cdev : nullptr;
+            return;
+        }
+        (void)hipGetLastError();
+        if (b <= a) return;
+        void* va = reinterpret_cast<void*>(a);
+        if (hipHostRegister(va, b - a, mapped ? hipHostRegisterMapped : hipHostRegisterDefault) !=
+            hipSuccess) {
+            (void)hipGetLastError();
+            return;
+        }
+        base = va;
+        lo = a;
+        hi = b;
+        if (mapped && hipHostGetDevicePointer(&dev, va, 0) != hipSuccess) {
+            dev = nullptr;
+            (void)hipGetLastError();
+        }
     }
     ~HostPin()
     {
@@ -596,6 +633,89 @@ struct HostPin {
     HostPin(const HostPin&) = delete;
     HostPin& operator=(const HostPin&) = delete;
 };
+
+// Device -> host bytes of a host call: the part inside the pinned range by a
+// copy kernel into its device address (the GPU's own stores over PCIe, so it
+// runs beside the SDMA upload) or else the runtime's copy engine; the parts
+// outside it (partial pages at the buffer's ends, or no pin) by the runtime's
+// pageable copy.
+hipError_t download(const HostPin* pin, void* host, const void* dev, size_t bytes, hipStream_t s)
+{
+    const uintptr_t h0 = reinterpret_cast<uintptr_t>(host), h1 = h0 + bytes;
+    const uintptr_t m0 = pin && pin->hi > pin->lo ? std::max(h0, pin->lo) : h1;
+    const uintptr_t m1 = pin && pin->hi > pin->lo ? std::min(h1, pin->hi) : h1;
+    const uint8_t* d = static_cast<const uint8_t*>(dev);
+    hipError_t e = hipSuccess;
+    auto copy = [&](uintptr_t a, uintptr_t b) {
+        if (b > a && e == hipSuccess)
+            e = hipMemcpyAsync(reinterpret_cast<void*>(a), d + (a - h0), b - a, hipMemcpyDeviceToHost, s);
+    };
+    if (m1 <= m0) {
+        copy(h0, h1);
+        return e;
+    }
+    copy(h0, m0);
+    if (e == hipSuccess) {
+        const uint8_t* src = d + (m0 - h0);
+        uint8_t* hd = pin->dev ? static_cast<uint8_t*>(pin->dev) + (m0 - pin->lo) : nullptr;
+        if (hd && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(hd)) & 3u) == 0)
+            e = dcte::launch_copy_to_host(src, hd, m1 - m0, s);
+        else
+            copy(m0, m1);
+    }
+    copy(m1, h1);
+    return e;
+}
+
+// Host -> device rows (a 2-D copy: `rows` rows of `width` bytes, host row
+// pitch spitch, device pitch dpitch), split so that every copy lies either
+// inside the pinned range [lo, hi) or outside it: the rows inside go as one
+// 2-D copy, the rows before / after it as pageable 2-D copies, a row that
+// straddles lo or hi as two 1-D pieces.
+hipError_t upload_rows(const HostPin* pin, uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch,
+                       size_t width, size_t rows, hipStream_t s)
+{
+    if (rows == 0 || width == 0) return hipSuccess;
+    auto copy2d = [&](size_t r0, size_t r1) -> hipError_t {
+        if (r1 <= r0) return hipSuccess;
+        return hipMemcpy2DAsync(dst + r0 * dpitch, dpitch, src + r0 * spitch, spitch, width, r1 - r0,
+                                hipMemcpyHostToDevice, s);
+    };
+    if (!pin || pin->hi <= pin->lo) return copy2d(0, rows);
+    const uintptr_t s0 = reinterpret_cast<uintptr_t>(src);
+    auto start = [&](size_t r) { return s0 + r * spitch; };
+    // first row starting at or after lo, first row ending after hi
+    size_t r1 = pin->lo <= s0 ? 0 : (size_t)((pin->lo - s0 + spitch - 1) / spitch);
+    size_t r2 = pin->hi < s0 + width ? 0 : (size_t)((pin->hi - s0 - width) / spitch) + 1;
+    r1 = std::min(r1, rows);
+    r2 = std::min(std::max(r2, r1), rows);
+    hipError_t e = hipSuccess;
+    auto piece = [&](size_t r, uintptr_t a, uintptr_t b) {   // bytes [a, b) of host row r, split at lo, hi
+        const uintptr_t cuts[4] = {a, std::min(std::max(pin->lo, a), b), std::min(std::max(pin->hi, a), b), b};
+        for (int k = 0; k < 3 && e == hipSuccess; k++)
+            if (cuts[k + 1] > cuts[k])
+                e = hipMemcpyAsync(dst + r * dpitch + (cuts[k] - start(r)), reinterpret_cast<const void*>(cuts[k]),
+                                   cuts[k + 1] - cuts[k], hipMemcpyHostToDevice, s);
+    };
+    auto outside_rows = [&](size_t a, size_t b, uintptr_t cut) {   // rows [a, b); one may straddle cut
+        for (size_t r = a; r < b && e == hipSuccess;) {
+            const uintptr_t r_lo = start(r), r_hi = r_lo + width;
+            if (r_lo < cut && r_hi > cut) {
+                piece(r, r_lo, r_hi);
+                r++;
+            } else {
+                size_t q = r + 1;   // a run of rows that do not straddle
+                while (q < b && !(start(q) < cut && start(q) + width > cut)) q++;
+                e = copy2d(r, q);
+                r = q;
+            }
+        }
+    };
+    outside_rows(0, r1, pin->lo);
+    if (e == hipSuccess) e = copy2d(r1, r2);
+    if (e == hipSuccess) outside_rows(r2, rows, pin->hi);
+    return e;
+}
 
 #ifndef DCTE_CHUNK_ROWS
 #define DCTE_CHUNK_ROWS 1024   // A/B: 22.4 ms per 16384^2 RGB frame vs 23.1 at 2048 (profiles/r02/host_chunks.jsonl)
@@ -647,7 +767,8 @@ int reset_refined(dcte_ctx* ctx, Device& d, int w, int rows, int n, int sem)
 // takes a strip of source COLUMNS (= transposed rows) plus halo, transposes
 // it in HBM and maps it (one chunk).
 int map_bands(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride, int n,
-              float edges, float textures, int sem, int transposed, float* host_out, int* used)
+              float edges, float textures, int sem, int transposed, float* host_out, int* used,
+              const HostPin* pin_in = nullptr, const HostPin* pin_out = nullptr)
 {
     const int W = transposed ? h : w, H = transposed ? w : h;   // mapped frame
     const int G = (int)ctx->devs.size() < H ? (int)ctx->devs.size() : H;
@@ -673,8 +794,7 @@ int map_bands(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t ro
         if (transposed) {
             // source columns [lo, hi] of all h rows -> (h x cols) strip -> transpose
             const size_t sw = (size_t)(hi - lo + 1) * bpp;
-            DCTE_HIP(ctx, hipMemcpy2DAsync(d.d_in, sw, px + (size_t)lo * bpp, rowstride, sw, h,
-                                           hipMemcpyHostToDevice, d.stream));
+            DCTE_HIP(ctx, upload_rows(pin_in, d.d_in, sw, px + (size_t)lo * bpp, rowstride, sw, h, d.stream));
             rc = ensure_buf(ctx, (void**)&d.d_tr, &d.tr_cap, in_bytes);
             if (rc) return rc;
             DCTE_HIP(ctx, dcte::launch_transpose_u8(d.d_in, (long long)sw, h, hi - lo + 1, bpp,
@@ -683,8 +803,7 @@ int map_bands(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t ro
                             n, edges, textures, sem, d.d_out, W, d.stream);
             if (rc) return rc;
             if (host_out)
-                DCTE_HIP(ctx, hipMemcpyAsync(host_out + (size_t)y0 * W, d.d_out, out_bytes,
-                                             hipMemcpyDeviceToHost, d.stream));
+                DCTE_HIP(ctx, download(pin_out, host_out + (size_t)y0 * W, d.d_out, out_bytes, d.stream));
             continue;
         }
         // at least 8 chunks of >= 256 rows where the band allows (a shorter
@@ -703,9 +822,9 @@ int map_bands(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t ro
             const int need = b - 1 + hr < H - 1 ? b - 1 + hr : H - 1;
             hipEvent_t ev_up = d.ev[2 * c], ev_map = d.ev[2 * c + 1];
             if (need > loaded) {
-                DCTE_HIP(ctx, hipMemcpy2DAsync(d.d_in + (size_t)(loaded + 1 - lo) * pitch, pitch,
-                                               px + (size_t)(loaded + 1) * rowstride, rowstride,
-                                               pitch, need - loaded, hipMemcpyHostToDevice, d.up));
+                DCTE_HIP(ctx, upload_rows(pin_in, d.d_in + (size_t)(loaded + 1 - lo) * pitch, pitch,
+                                          px + (size_t)(loaded + 1) * rowstride, rowstride, pitch,
+                                          (size_t)(need - loaded), d.up));
                 loaded = need;
             }
             DCTE_HIP(ctx, hipEventRecord(ev_up, d.up));
@@ -716,9 +835,8 @@ int map_bands(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t ro
             if (host_out) {
                 DCTE_HIP(ctx, hipEventRecord(ev_map, d.stream));
                 DCTE_HIP(ctx, hipStreamWaitEvent(d.down, ev_map, 0));
-                DCTE_HIP(ctx, hipMemcpyAsync(host_out + (size_t)a * W, d.d_out + (size_t)(a - y0) * W,
-                                             sizeof(float) * (size_t)W * (size_t)(b - a),
-                                             hipMemcpyDeviceToHost, d.down));
+                DCTE_HIP(ctx, download(pin_out, host_out + (size_t)a * W, d.d_out + (size_t)(a - y0) * W,
+                                       sizeof(float) * (size_t)W * (size_t)(b - a), d.down));
             }
         }
     }
@@ -734,7 +852,8 @@ int map_bands(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t ro
 // column strips), each downloaded as soon as it is mapped -- one upload for
 // both orientations, and the downloads of both maps back to back on d.down.
 int map_pipeline_one(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride,
-                     int n, float edges, float textures, int sem, float* out, float* out_t)
+                     int n, float edges, float textures, int sem, float* out, float* out_t,
+                     const HostPin* pin_in, const HostPin* pin_out, const HostPin* pin_out_t)
 {
     Device& d = ctx->devs[0];
     int hl, hr;
@@ -766,9 +885,9 @@ int map_pipeline_one(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, si
         const int need = out ? (b - 1 + hr < h - 1 ? b - 1 + hr : h - 1) : b - 1;
         hipEvent_t ev_up = d.ev[2 * c], ev_map = d.ev[2 * c + 1];
         if (need > loaded) {
-            DCTE_HIP(ctx, hipMemcpy2DAsync(d.d_in + (size_t)(loaded + 1) * pitch, pitch,
-                                           px + (size_t)(loaded + 1) * rowstride, rowstride, pitch,
-                                           need - loaded, hipMemcpyHostToDevice, d.up));
+            DCTE_HIP(ctx, upload_rows(pin_in, d.d_in + (size_t)(loaded + 1) * pitch, pitch,
+                                      px + (size_t)(loaded + 1) * rowstride, rowstride, pitch,
+                                      (size_t)(need - loaded), d.up));
             loaded = need;
         }
         DCTE_HIP(ctx, hipEventRecord(ev_up, d.up));
@@ -779,9 +898,8 @@ int map_pipeline_one(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, si
         if (rc) return rc;
         DCTE_HIP(ctx, hipEventRecord(ev_map, d.stream));
         DCTE_HIP(ctx, hipStreamWaitEvent(d.down, ev_map, 0));
-        DCTE_HIP(ctx, hipMemcpyAsync(out + (size_t)a * w, d.d_out + (size_t)a * w,
-                                     sizeof(float) * (size_t)w * (size_t)(b - a),
-                                     hipMemcpyDeviceToHost, d.down));
+        DCTE_HIP(ctx, download(pin_out, out + (size_t)a * w, d.d_out + (size_t)a * w,
+                               sizeof(float) * (size_t)w * (size_t)(b - a), d.down));
     }
     if (!out_t) return DCTE_OK;
     // the whole frame is in once the last upload is (ordered after every copy on d.up)
@@ -798,9 +916,8 @@ int map_pipeline_one(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, si
         hipEvent_t ev_map = d.ev[2 * nch0 + c];
         DCTE_HIP(ctx, hipEventRecord(ev_map, d.stream));
         DCTE_HIP(ctx, hipStreamWaitEvent(d.down, ev_map, 0));
-        DCTE_HIP(ctx, hipMemcpyAsync(out_t + (size_t)a * h, d.d_out2 + (size_t)a * h,
-                                     sizeof(float) * (size_t)h * (size_t)(b - a),
-                                     hipMemcpyDeviceToHost, d.down));
+        DCTE_HIP(ctx, download(pin_out_t, out_t + (size_t)a * h, d.d_out2 + (size_t)a * h,
+                               sizeof(float) * (size_t)h * (size_t)(b - a), d.down));
     }
     return DCTE_OK;
 }
@@ -817,7 +934,9 @@ void drain(dcte_ctx* ctx, int G)
     }
 }
 
-int normalize_bands(dcte_ctx* ctx, int w, int h, int mode, int channels, uint8_t* out, int G);
+struct HostPin;
+int normalize_bands(dcte_ctx* ctx, int w, int h, int mode, int channels, uint8_t* out, int G,
+                    const HostPin* pin_out);
 
 int sync_bands(dcte_ctx* ctx, int G)
 {
@@ -865,6 +984,8 @@ int dcte_create(dcte_ctx** out, int ngpus, unsigned flags)
     for (int i = 0; i < ngpus; i++) ctx->devs[i].id = same ? 0 : i;
     const char* tau = getenv("DCTE_TIE_TAU");
     if (tau && *tau) ctx->tie_tau = atof(tau);
+    const char* pin = getenv("DCTE_PIN_HOST");       // DCTE_OPT_PIN_HOST's initial value (diagnostics)
+    if (pin && *pin) ctx->pin_mib = atof(pin);
     *out = ctx;
     return DCTE_OK;
 }
@@ -952,6 +1073,9 @@ int dcte_set_option(dcte_ctx* ctx, int option, double value)
         return DCTE_OK;
     case DCTE_OPT_EXACT:
         ctx->exact = value != 0;
+        return DCTE_OK;
+    case DCTE_OPT_D2H_KERNEL:
+        ctx->d2h_kernel = value != 0;
         return DCTE_OK;
     default: return DCTE_EINVAL;
     }
@@ -1592,15 +1716,18 @@ int dcte_energy_map(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, siz
     DCTE_ARG(ctx, px && out && valid_n(n) && valid_sem_bpp(semantics, bpp) && w > 0 && h > 0);
     DCTE_ARG(ctx, rowstride >= (size_t)w * bpp);
     ctx->last_refined = 0;
+    const bool one = ctx->devs.size() == 1;
     HostPin pin_in(ctx, px, (size_t)(h - 1) * rowstride + (size_t)w * bpp);
-    HostPin pin_out(ctx, out, sizeof(float) * (size_t)w * (size_t)h);
+    HostPin pin_out(ctx, out, sizeof(float) * (size_t)w * (size_t)h, one && ctx->d2h_kernel);
     int G = 0;
     int rc;
-    if (transposed && ctx->devs.size() == 1) {   // chunked: the map's download overlaps its launches
+    if (transposed && one) {   // chunked: the map's download overlaps its launches
         G = 1;
-        rc = map_pipeline_one(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, nullptr, out);
+        rc = map_pipeline_one(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, nullptr, out,
+                              &pin_in, nullptr, &pin_out);
     } else {
-        rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, transposed, out, &G);
+        rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, transposed, out, &G,
+                       &pin_in, &pin_out);
     }
     if (rc) {
         drain(ctx, G);              // nothing in flight may still use px / out
@@ -1627,9 +1754,10 @@ int dcte_energy_map2(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, si
     }
     ctx->last_refined = 0;
     HostPin pin_in(ctx, px, (size_t)(h - 1) * rowstride + (size_t)w * bpp);
-    HostPin pin_out(ctx, out, out ? sizeof(float) * (size_t)w * (size_t)h : 0);
-    HostPin pin_out_t(ctx, out_t, out_t ? sizeof(float) * (size_t)w * (size_t)h : 0);
-    int rc = map_pipeline_one(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, out, out_t);
+    HostPin pin_out(ctx, out, out ? sizeof(float) * (size_t)w * (size_t)h : 0, ctx->d2h_kernel);
+    HostPin pin_out_t(ctx, out_t, out_t ? sizeof(float) * (size_t)w * (size_t)h : 0, ctx->d2h_kernel);
+    int rc = map_pipeline_one(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, out, out_t,
+                              &pin_in, &pin_out, &pin_out_t);
     if (rc) {
         drain(ctx, 1);              // nothing in flight may still use px / out / out_t
         return rc;
@@ -1648,10 +1776,11 @@ int dcte_energy_image_u8(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp
     ctx->last_refined = 0;
     int G = 0;
     HostPin pin_in(ctx, px, (size_t)(h - 1) * rowstride + (size_t)w * bpp);
-    HostPin pin_out(ctx, out, (size_t)w * (size_t)h * (size_t)channels);
+    HostPin pin_out(ctx, out, (size_t)w * (size_t)h * (size_t)channels,
+                    ctx->devs.size() == 1 && ctx->d2h_kernel);
     int rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, 0, nullptr,
-                       &G);
-    if (rc == DCTE_OK) rc = normalize_bands(ctx, w, h, mode, channels, out, G);
+                       &G, &pin_in);
+    if (rc == DCTE_OK) rc = normalize_bands(ctx, w, h, mode, channels, out, G, &pin_out);
     if (rc) {
         drain(ctx, G);              // nothing in flight may still use px / out
         return rc;
@@ -1664,7 +1793,8 @@ int dcte_energy_image_u8(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp
 namespace {
 
 // energy_image_u8, second half: global min/max over the band maps, then u8
-int normalize_bands(dcte_ctx* ctx, int w, int h, int mode, int channels, uint8_t* out, int G)
+int normalize_bands(dcte_ctx* ctx, int w, int h, int mode, int channels, uint8_t* out, int G,
+                    const HostPin* pin_out)
 {
     int rc;
     // per-band min/max, reduced on the host (2 floats per device)
@@ -1690,8 +1820,7 @@ int normalize_bands(dcte_ctx* ctx, int w, int h, int mode, int channels, uint8_t
         rc = ensure_buf(ctx, (void**)&d.d_u8, &d.u8_cap, npx * channels);
         if (rc) return rc;
         DCTE_HIP(ctx, dcte::launch_to_u8(d.d_out, (long long)npx, d.d_minmax, mode, channels, d.d_u8, d.stream));
-        DCTE_HIP(ctx, hipMemcpyAsync(out + (size_t)y0 * w * channels, d.d_u8, npx * channels,
-                                     hipMemcpyDeviceToHost, d.stream));
+        DCTE_HIP(ctx, download(pin_out, out + (size_t)y0 * w * channels, d.d_u8, npx * channels, d.stream));
     }
     return DCTE_OK;
 }

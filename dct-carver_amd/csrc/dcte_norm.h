@@ -18,4 +18,13 @@ hipError_t launch_to_u8(const float* e, long long n, const float* minmax, int mo
 hipError_t launch_transpose_u8(const uint8_t* src, long long src_pitch, int rows, int cols, int bpp,
                                uint8_t* dst, long long dst_pitch, hipStream_t s);
 
+// bytes from device memory to page-locked host memory mapped into the device
+// (host_dev = hipHostGetDevicePointer of the host buffer) by a kernel: the
+// GPU's own stores over PCIe, no SDMA engine.  An SDMA upload and a
+// kernel-driven download run at the same time (16384^2 frame up + map down:
+// 21.3 ms), where two SDMA copies in opposite directions were serialised by
+// the runtime on some runs (32.9 ms) -- tools/zc_probe.py,
+// profiles/r06/zc_probe.jsonl.  src and host_dev must be 4-byte aligned.
+hipError_t launch_copy_to_host(const void* src, void* host_dev, size_t bytes, hipStream_t s);
+
 }  // namespace dcte

@@ -39,6 +39,7 @@ DCTE_OPT_TSTAMP_BUF = 7
 DCTE_OPT_LEGACY_8 = 8
 DCTE_OPT_FAIL_INJECT = 9
 DCTE_OPT_EXACT = 10
+DCTE_OPT_D2H_KERNEL = 11
 DCTE_NORM_LQR = 0
 DCTE_NORM_PREVIEW = 1
 DCTE_CREATE_SAME_DEVICE = 1

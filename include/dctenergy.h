@@ -124,6 +124,14 @@ extern "C" {
                                refined in fp64 too.  0 = the fp32 map with the
                                tie refinement (default; <= 1e-5 relative). */
 
+#define DCTE_OPT_D2H_KERNEL 11 /* host entry points on one device: 1 (default)
+                               = the maps go down through a copy kernel that
+                               writes the page-locked output directly (the
+                               GPU's own stores over PCIe, beside the SDMA
+                               upload); 0 = the runtime's copy engine, which
+                               on some runs serialised the two directions
+                               (38 instead of 22 ms at 16384^2) */
+
 typedef struct dcte_ctx dcte_ctx;
 
 int dcte_abi_version(void);

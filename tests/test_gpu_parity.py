@@ -621,6 +621,66 @@ def test_multi_device_host_path_on_one_gpu(ctx, G):
                                       many.energy_image_u8(img, n, 0.3, 0.7, mode, ch)), (n, mode)
 
 
+def test_kernel_download_equals_copy_engine(ctx):
+    """DCTE_OPT_D2H_KERNEL (default 1): the host entry points' maps come down
+    through a copy kernel writing the page-locked output; bit-identical to
+    the runtime's copies (0) -- aligned and 4-byte-offset outputs (the
+    dword path), both orientations, dcte_energy_map2, frames above and below
+    the 1 MiB page-locking threshold, and a caller-pinned output."""
+    import torch
+    rng = np.random.default_rng(11)
+    for h, w in ((1003, 777), (100, 300), (2050, 129)):
+        img = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        want = {}
+        for kern in (0, 1):
+            ctx.set_option(dctenergy.DCTE_OPT_D2H_KERNEL, kern)
+            a = ctx.energy_map(img, 8, 0.3, 0.7)
+            b = ctx.energy_map(img, 16, 0.3, 0.7, transposed=True)
+            o, ot = ctx.energy_map2(img, 4, 0.3, 0.7)
+            raw = np.zeros(h * w * 4 + 8, np.uint8)        # a float map 4 bytes off 16-byte alignment
+            off = raw[4:4 + h * w * 4].view(np.float32).reshape(h, w)
+            ctx.energy_map(img, 8, 0.3, 0.7, out=off)
+            pinned = torch.empty((h, w), dtype=torch.float32, pin_memory=True).numpy()
+            ctx.energy_map(img, 8, 0.3, 0.7, out=pinned)
+            want[kern] = (a, b, o, ot, off.copy(), pinned.copy())
+        for x, y in zip(want[0], want[1]):
+            assert np.array_equal(x, y), (h, w)
+        assert np.array_equal(want[1][0], want[1][4]) and np.array_equal(want[1][0], want[1][5])
+    ctx.set_option(dctenergy.DCTE_OPT_D2H_KERNEL, 1)
+
+
+def test_host_path_split_at_pinned_pages(ctx):
+    """The host path page-locks only the whole pages inside the caller's
+    buffers and copies the partial pages at their ends through the runtime's
+    pageable path (dcte_capi.cpp HostPin / upload_rows / download): frames at
+    odd offsets with padded row strides (rows straddling the first and last
+    locked page), grey layers whose pageable frame shares pages with a
+    locked map (the 3 x 100003 case that faulted with exact-byte
+    registration), u8 layers and both orientations -- all bit-equal to the
+    same calls without page-locking."""
+    rng = np.random.default_rng(3)
+    cases = [(3, 100003, 1, 0, 0), (700, 511, 3, 13, 4093), (1031, 333, 3, 1, 7), (257, 4099, 1, 5, 1)]
+    for h, w, bpp, pad, off in cases:
+        rs = w * bpp + pad
+        buf = np.zeros(off + h * rs + 64, np.uint8)
+        frame = np.lib.stride_tricks.as_strided(buf[off:], (h, w, bpp), (rs, bpp, 1)) if bpp > 1 else \
+            np.lib.stride_tricks.as_strided(buf[off:], (h, w), (rs, 1))
+        frame[...] = rng.integers(0, 256, frame.shape, dtype=np.uint8)
+        got = {}
+        for pin in (0, 1):
+            ctx.set_option(dctenergy.DCTE_OPT_PIN_HOST, pin)
+            r = []
+            for n in (8, 16):
+                out = np.zeros(h * w + 3, np.float32)[1:1 + h * w].reshape(h, w)   # 4 bytes off 16
+                r.append(ctx.energy_map(frame, n, 0.3, 0.7, out=out).copy())
+                r.append(ctx.energy_map(frame, n, 0.3, 0.7, transposed=True))
+                r.append(ctx.energy_image_u8(frame, n, 0.3, 0.7, dctenergy.DCTE_NORM_PREVIEW, 3))
+            got[pin] = r
+        ctx.set_option(dctenergy.DCTE_OPT_PIN_HOST, 1)
+        for a, b in zip(got[0], got[1]):
+            assert np.array_equal(a, b), (h, w, bpp, pad, off)
+
+
 def test_host_buffers_sharing_pages(ctx):
     """Frame and output packed into one allocation, so they share a page at
     unaligned addresses (the page-locking of the host path registers exactly
