@@ -723,8 +723,23 @@ hipError_t upload_rows(const HostPin* pin, uint8_t* dst, size_t dpitch, const ui
 #ifndef DCTE_MAX_CHUNKS
 #define DCTE_MAX_CHUNKS 16
 #endif
+#ifndef DCTE_CHUNK_SPLIT
+#define DCTE_CHUNK_SPLIT 8      // at least this many chunks per band ...
+#endif
+#ifndef DCTE_CHUNK_MIN_ROWS
+#define DCTE_CHUNK_MIN_ROWS 256 // ... of at least this many rows
+#endif
 constexpr int kChunkRows = DCTE_CHUNK_ROWS;   // host path: output rows per pipeline chunk
 constexpr int kMaxChunks = DCTE_MAX_CHUNKS;
+
+// rows per chunk of a host-path band of `rows` rows: at least DCTE_CHUNK_SPLIT
+// chunks where the band allows (a shorter first upload and last download: the
+// pipeline's ramp), at least DCTE_CHUNK_MIN_ROWS rows, at most kChunkRows
+int chunk_rows(int rows)
+{
+    int crows = rows / DCTE_CHUNK_SPLIT;
+    return crows < DCTE_CHUNK_MIN_ROWS ? DCTE_CHUNK_MIN_ROWS : (crows > kChunkRows ? kChunkRows : crows);
+}
 
 int ensure_pipe(dcte_ctx* ctx, Device& d, size_t nev)
 {
@@ -806,10 +821,7 @@ int map_bands(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t ro
                 DCTE_HIP(ctx, download(pin_out, host_out + (size_t)y0 * W, d.d_out, out_bytes, d.stream));
             continue;
         }
-        // at least 8 chunks of >= 256 rows where the band allows (a shorter
-        // first upload and last download: the pipeline's ramp)
-        int crows = (y1 - y0) / 8;
-        crows = crows < 256 ? 256 : (crows > kChunkRows ? kChunkRows : crows);
+        const int crows = chunk_rows(y1 - y0);
         int nch = (y1 - y0 + crows - 1) / crows;
         nch = nch < 1 ? 1 : (nch > kMaxChunks ? kMaxChunks : nch);
         rc = ensure_pipe(ctx, d, 2 * (size_t)nch);
@@ -871,8 +883,7 @@ int map_pipeline_one(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, si
     if ((rc = reset_refined(ctx, d, w, h, n, sem))) return rc;
     // at least 8 chunks of >= 256 rows where the frame allows (map_bands)
     auto chunks = [](int rows) {
-        int crows = rows / 8;
-        crows = crows < 256 ? 256 : (crows > kChunkRows ? kChunkRows : crows);
+        const int crows = chunk_rows(rows);
         int nch = (rows + crows - 1) / crows;
         return nch < 1 ? 1 : (nch > kMaxChunks ? kMaxChunks : nch);
     };
