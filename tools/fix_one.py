@@ -18,7 +18,7 @@ def main():
     ap.add_argument("--n", type=int, default=8)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--lib", default=None)
-    ap.add_argument("--tau", type=float, default=4e-6)
+    ap.add_argument("--tau", type=float, default=-1, help="DCTE_OPT_TIE_TAU (< 0: the per-N defaults)")
     a = ap.parse_args()
     if a.lib:
         os.environ["DCTE_LIB"] = os.path.abspath(a.lib)
