@@ -927,6 +927,15 @@ __device__ __forceinline__ void refine_group(const double* lum, int LW, int at, 
 #ifndef DCTE_DENSE_OVERSUB_MEMO8
 #define DCTE_DENSE_OVERSUB_MEMO8 2
 #endif
+// ... on launches of fewer pixels than DCTE_MEMO8_BIG_PX, 1: each wave then
+// walks more strips with its memo warm -- 1 vs 2 (r06), the four grey frames
+// of tools/fix_study.py summed: 2048^2 -8 %, 4096^2 -12 % (line art -18 %,
+// the 8-px grid -17 %; preview -12 %), 6144^2 -4 %, 8192^2 -2 %, 11584^2
+// -3 %, but 16384^2 +2 % (liblqr and preview; profiles/r06/memo_oversub1_ab.jsonl,
+// memo_oversub1_sizes.jsonl)
+#ifndef DCTE_MEMO8_BIG_PX
+#define DCTE_MEMO8_BIG_PX 192000000LL
+#endif
 // grey layers at N <= 4 fit 128 VGPRs: 4 waves per SIMD (the LDS allows them)
 #ifndef DCTE_FIX_MINW
 #define DCTE_FIX_MINW 4
@@ -2476,7 +2485,9 @@ static hipError_t launch_fix_tiles_t(const TileFixParams& p, hipStream_t s)
         const long long most = kDenseFlat<N, SEM>
                                    ? ((long long)nstrips * 64 * p.m.tile_h + kDenseBatch16 - 1) / kDenseBatch16
                                    : nstrips;
-        const long long dmax = (long long)resident * (N <= 8 && BPP == 1 ? (N == 8 ? DCTE_DENSE_OVERSUB_MEMO8 : DCTE_DENSE_OVERSUB_MEMO)
+        const long long npx = (long long)p.m.w * ((p.m.y1 - p.m.y0) + (p.m.yb1 - p.m.yb0));
+        const int memo8 = npx < DCTE_MEMO8_BIG_PX ? 1 : DCTE_DENSE_OVERSUB_MEMO8;
+        const long long dmax = (long long)resident * (N <= 8 && BPP == 1 ? (N == 8 ? memo8 : DCTE_DENSE_OVERSUB_MEMO)
                                                                      : DCTE_DENSE_OVERSUB);
         const int dblocks = (int)(most < dmax ? most : dmax);
         TileFixParams q = p;

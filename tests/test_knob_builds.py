@@ -40,6 +40,7 @@ KNOBS = {
     "DCTE_DENSE_OVERSUB": ("dcte_kernels.hip", "1"),
     "DCTE_DENSE_OVERSUB_MEMO": ("dcte_kernels.hip", "16"),
     "DCTE_DENSE_OVERSUB_MEMO8": ("dcte_kernels.hip", "4"),
+    "DCTE_MEMO8_BIG_PX": ("dcte_kernels.hip", "0LL"),
     "DCTE_MEMO_SLOTS": ("dcte_kernels.hip", "64"),
     "DCTE_MEMO_WAYS": ("dcte_kernels.hip", "1"),
     "DCTE_EX_TILE_H": ("dcte_exact.hip", "64"),
@@ -52,6 +53,8 @@ KNOBS = {
     "DCTE_DP_NB": ("dcte_dp.hip", "2"),
     "DCTE_CHUNK_ROWS": ("dcte_capi.cpp", "2048"),
     "DCTE_MAX_CHUNKS": ("dcte_capi.cpp", "8"),
+    "DCTE_CHUNK_SPLIT": ("dcte_capi.cpp", "4"),
+    "DCTE_CHUNK_MIN_ROWS": ("dcte_capi.cpp", "64"),
 }
 
 _HEADER_GUARDS = {"DCTE_KERNELS_H", "DCTE_LUMA_H", "DCTE_NORM_H", "DCTE_PIXEL_H", "DCTE_MATH_H",
