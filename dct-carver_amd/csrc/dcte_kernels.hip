@@ -1034,7 +1034,9 @@ __device__ __forceinline__ bool rgb_line_grey(const uint32_t (&wd)[K])
 // all grey) the probe's 56-dword row loads, loaded again for every miss, cost
 // more than the hits save -- with this hash and 3 waves per SIMD: grey line
 // art stored as RGB +7 %, colour strokes +22 %, dots +17 %
-// (profiles/r04/memo_ab.jsonl).
+// (profiles/r04/memo_ab.jsonl); with r05's two ways (r06, 1-3 waves per
+// SIMD): line art RGB -1.6 %, colour strokes +28 %, dots +18 %
+// (profiles/r06/memo_rgb_ab.jsonl).
 // 128 slots (8.7 KB with the queue, the block's LDS 11 KB: 3 waves per SIMD
 // still fit): vs 64 the grid 1.50 -> 1.39 ms, line art 0.269 -> 0.265, dots
 // -7 %; 256 costs occupancy (grid 1.62) (profiles/r04/memo_slots_ab.jsonl).
