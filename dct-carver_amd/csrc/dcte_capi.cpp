@@ -131,6 +131,12 @@ struct dcte_ctx {
     int fail_inject = 0;            // DCTE_OPT_FAIL_INJECT (tests of the error paths)
     bool exact = false;             // DCTE_OPT_EXACT
     bool d2h_kernel = true;         // DCTE_OPT_D2H_KERNEL
+    // page-locked staging of the host-call bytes no registration covers
+    // (HostPin), per role: 0 the frame, 1 the map / layer, 2 map2's second map
+    struct Stage {
+        uint8_t* p = nullptr;
+        size_t cap = 0;
+    } stage[3];
     std::vector<ProfEvent> prof;
     long long last_refined = 0;
     std::string last_error;
@@ -575,56 +581,106 @@ bool valid_norm(int mode, int channels)
     return (mode == DCTE_NORM_LQR || mode == DCTE_NORM_PREVIEW) && channels >= 1 && channels <= 4;
 }
 
-// Page-locks a caller buffer for the duration of a host call (RAII).  A
-// buffer that is already pinned, or that the runtime refuses, stays as it is:
-// pinning only lets the chunk copies overlap, it never changes results.
-// Only the WHOLE pages inside the caller's bytes are registered, [lo, hi):
-// a page the buffer shares with a neighbour is never locked by us.  (r05
-// registered exactly the caller's bytes, after a page-rounded range had made
-// the runtime refuse copies into a neighbour -- tools/pin_probe.cpp; but the
-// runtime locks whole pages, and a pageable copy of a neighbour sharing the
-// first or last page -- the runtime pins such copies on the fly and unpins
-// them afterwards -- then left the download into our buffer faulting
-// (hipErrorIllegalAddress at the sync: test_extreme_aspect_ratios, a
-// 3 x 100003 grey frame whose 300 KB frame copy is pageable and whose 1.2 MB
-// map is registered).)  The copies split at lo and hi: the partial pages at
-// either end go through the runtime's pageable path (upload_rows, download).
+// Page-locks a caller buffer for the duration of a host call (RAII), so that
+// no copy of the call goes through the runtime's pageable path.  Only the
+// WHOLE pages inside the caller's bytes are registered, [lo, hi), and only for
+// buffers of at least DCTE_OPT_PIN_HOST MiB: a page the buffer shares with a
+// neighbour is never locked by us.  (r05 registered exactly the caller's
+// bytes, after a page-rounded range had made the runtime refuse copies into a
+// neighbour -- tools/pin_probe.cpp; but the runtime locks whole pages, and a
+// pageable copy of a neighbour sharing the first or last page -- the runtime
+// pins such copies on the fly and unpins them afterwards -- then left the
+// download into our buffer faulting: hipErrorIllegalAddress at the sync of
+// test_extreme_aspect_ratios, a 3 x 100003 grey frame whose 300 KB frame copy
+// was pageable and whose 1.2 MB map was registered.)  The bytes outside
+// [lo, hi) -- the partial pages at either end, or the whole of a small buffer
+// -- are staged through the context's page-locked arena for the role
+// (dcte_ctx::stage): an input's are copied there when the pin is made, an
+// output's are copied back by commit() after the call's streams are drained.
+// (r06: pageable copies of one frame on several streams at once -- the band
+// uploads of a multi-device context, whose halo rows share pages, or the
+// transposed strips, which all read every row -- faulted the same way,
+// test_exact_multi_device_host_path, profiles/r06/multi_device_pageable_fault.log.)
 // With `mapped`, also the device address of lo (dev) for a copy kernel to
 // write into; a caller-pinned buffer (hipHostMalloc, or registered by the
-// caller) is used whole, with its own device address.
+// caller) is used whole, with its own device address.  DCTE_OPT_PIN_HOST <= 0:
+// no registration, every byte staged.  Only when the arena cannot be allocated
+// do the outside bytes take the runtime's pageable path.
 struct HostPin {
     void* base = nullptr;            // what we registered (unregistered at the end)
-    uintptr_t lo = 0, hi = 0;        // pinned host range
+    uintptr_t p0 = 0, p1 = 0;        // the caller's bytes
+    uintptr_t lo = 0, hi = 0;        // the pinned part (registered or caller-pinned)
     void* dev = nullptr;             // device address of lo (mapped), or null
-    HostPin(const dcte_ctx* ctx, const void* p, size_t bytes, bool mapped = false)
+    uint8_t* st = nullptr;           // staged [p0, lo) then [hi, p1), or null (pageable)
+    bool output = false;
+    HostPin(dcte_ctx* ctx, const void* p, size_t bytes, bool mapped, int role, bool is_output)
     {
-        if (!p || ctx->pin_mib <= 0 || (double)bytes < ctx->pin_mib * 1048576.0) return;
-        const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + 4095u) & ~(uintptr_t)4095u;
-        const uintptr_t b = (reinterpret_cast<uintptr_t>(p) + bytes) & ~(uintptr_t)4095u;
+        if (!p || bytes == 0) return;
+        output = is_output;
+        p0 = reinterpret_cast<uintptr_t>(p);
+        p1 = p0 + bytes;
         void* v = const_cast<void*>(p);
         // a caller-pinned buffer first (registering part of it would fail)
         void* cdev = nullptr;
         if (hipHostGetDevicePointer(&cdev, v, 0) == hipSuccess && cdev) {
-            lo = reinterpret_cast<uintptr_t>(p);
-            hi = lo + bytes;
+            lo = p0;
+            hi = p1;
             dev = mapped ? cdev : nullptr;
             return;
         }
         (void)hipGetLastError();
-        if (b <= a) return;
-        void* va = reinterpret_cast<void*>(a);
-        if (hipHostRegister(va, b - a, mapped ? hipHostRegisterMapped : hipHostRegisterDefault) !=
-            hipSuccess) {
-            (void)hipGetLastError();
-            return;
+        lo = hi = p1;                                  // nothing registered: all staged
+        const uintptr_t a = (p0 + 4095u) & ~(uintptr_t)4095u, b = p1 & ~(uintptr_t)4095u;
+        if (ctx->pin_mib > 0 && (double)bytes >= ctx->pin_mib * 1048576.0 && b > a) {
+            void* va = reinterpret_cast<void*>(a);
+            if (hipHostRegister(va, b - a, mapped ? hipHostRegisterMapped : hipHostRegisterDefault) ==
+                hipSuccess) {
+                base = va;
+                lo = a;
+                hi = b;
+                if (mapped && hipHostGetDevicePointer(&dev, va, 0) != hipSuccess) {
+                    dev = nullptr;
+                    (void)hipGetLastError();
+                }
+            } else {
+                (void)hipGetLastError();
+            }
         }
-        base = va;
-        lo = a;
-        hi = b;
-        if (mapped && hipHostGetDevicePointer(&dev, va, 0) != hipSuccess) {
-            dev = nullptr;
-            (void)hipGetLastError();
+        const size_t ns = (size_t)(lo - p0) + (size_t)(p1 - hi);
+        if (!ns) return;
+        auto& S = ctx->stage[role];
+        if (S.cap < ns) {                              // no copy of an earlier call is in flight
+            if (S.p) (void)hipHostFree(S.p);
+            S.p = nullptr;
+            S.cap = 0;
+            if (hipHostMalloc(reinterpret_cast<void**>(&S.p), ns, hipHostMallocDefault) != hipSuccess) {
+                (void)hipGetLastError();
+                S.p = nullptr;                         // the pageable path, as before r06
+                return;
+            }
+            S.cap = ns;
         }
+        st = S.p;
+        if (!output) {
+            memcpy(st, reinterpret_cast<const void*>(p0), lo - p0);
+            memcpy(st + (lo - p0), reinterpret_cast<const void*>(hi), p1 - hi);
+        }
+    }
+    // the host address to copy caller bytes [a, ...) outside [lo, hi) to /
+    // from: their staged copy (the piece must lie wholly before lo or wholly
+    // at or after hi), or the caller's own bytes when nothing is staged
+    uint8_t* outside(uintptr_t a) const
+    {
+        if (!st) return reinterpret_cast<uint8_t*>(a);
+        return a < lo ? st + (a - p0) : st + (lo - p0) + (a - hi);
+    }
+    // an output's staged bytes into the caller's buffer (after the streams
+    // are drained; a failed call leaves them untouched)
+    void commit() const
+    {
+        if (!output || !st) return;
+        memcpy(reinterpret_cast<void*>(p0), st, lo - p0);
+        memcpy(reinterpret_cast<void*>(hi), st + (lo - p0), p1 - hi);
     }
     ~HostPin()
     {
@@ -637,53 +693,56 @@ struct HostPin {
 // Device -> host bytes of a host call: the part inside the pinned range by a
 // copy kernel into its device address (the GPU's own stores over PCIe, so it
 // runs beside the SDMA upload) or else the runtime's copy engine; the parts
-// outside it (partial pages at the buffer's ends, or no pin) by the runtime's
-// pageable copy.
+// outside it (partial pages at the buffer's ends, a small buffer, or no pin)
+// into their staged copies (HostPin::outside).
 hipError_t download(const HostPin* pin, void* host, const void* dev, size_t bytes, hipStream_t s)
 {
     const uintptr_t h0 = reinterpret_cast<uintptr_t>(host), h1 = h0 + bytes;
-    const uintptr_t m0 = pin && pin->hi > pin->lo ? std::max(h0, pin->lo) : h1;
-    const uintptr_t m1 = pin && pin->hi > pin->lo ? std::min(h1, pin->hi) : h1;
+    const bool reg = pin && pin->hi > pin->lo;
+    const uintptr_t m0 = reg ? std::max(h0, pin->lo) : h1;
+    const uintptr_t m1 = reg ? std::min(h1, pin->hi) : h1;
     const uint8_t* d = static_cast<const uint8_t*>(dev);
     hipError_t e = hipSuccess;
-    auto copy = [&](uintptr_t a, uintptr_t b) {
+    auto copy = [&](uintptr_t a, uintptr_t b, bool inside) {
         if (b > a && e == hipSuccess)
-            e = hipMemcpyAsync(reinterpret_cast<void*>(a), d + (a - h0), b - a, hipMemcpyDeviceToHost, s);
+            e = hipMemcpyAsync(inside || !pin ? reinterpret_cast<void*>(a) : pin->outside(a), d + (a - h0), b - a,
+                               hipMemcpyDeviceToHost, s);
     };
-    if (m1 <= m0) {
-        copy(h0, h1);
+    if (m1 <= m0) {                                    // wholly before lo, or at / after hi
+        copy(h0, h1, false);
         return e;
     }
-    copy(h0, m0);
+    copy(h0, m0, false);
     if (e == hipSuccess) {
         const uint8_t* src = d + (m0 - h0);
         uint8_t* hd = pin->dev ? static_cast<uint8_t*>(pin->dev) + (m0 - pin->lo) : nullptr;
         if (hd && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(hd)) & 3u) == 0)
             e = dcte::launch_copy_to_host(src, hd, m1 - m0, s);
         else
-            copy(m0, m1);
+            copy(m0, m1, true);
     }
-    copy(m1, h1);
+    copy(m1, h1, false);
     return e;
 }
 
 // Host -> device rows (a 2-D copy: `rows` rows of `width` bytes, host row
 // pitch spitch, device pitch dpitch), split so that every copy lies either
 // inside the pinned range [lo, hi) or outside it: the rows inside go as one
-// 2-D copy, the rows before / after it as pageable 2-D copies, a row that
-// straddles lo or hi as two 1-D pieces.
+// 2-D copy, the rows before / after it as 2-D copies from their staged bytes,
+// a row that straddles lo or hi as 1-D pieces.
 hipError_t upload_rows(const HostPin* pin, uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch,
                        size_t width, size_t rows, hipStream_t s)
 {
     if (rows == 0 || width == 0) return hipSuccess;
-    auto copy2d = [&](size_t r0, size_t r1) -> hipError_t {
-        if (r1 <= r0) return hipSuccess;
-        return hipMemcpy2DAsync(dst + r0 * dpitch, dpitch, src + r0 * spitch, spitch, width, r1 - r0,
-                                hipMemcpyHostToDevice, s);
-    };
-    if (!pin || pin->hi <= pin->lo) return copy2d(0, rows);
     const uintptr_t s0 = reinterpret_cast<uintptr_t>(src);
     auto start = [&](size_t r) { return s0 + r * spitch; };
+    // rows [r0, r1) as one 2-D copy, from the caller's bytes (inside) or their staged copy
+    auto copy2d = [&](size_t r0, size_t r1, bool inside) -> hipError_t {
+        if (r1 <= r0) return hipSuccess;
+        const uint8_t* from = inside || !pin ? src + r0 * spitch : pin->outside(start(r0));
+        return hipMemcpy2DAsync(dst + r0 * dpitch, dpitch, from, spitch, width, r1 - r0, hipMemcpyHostToDevice, s);
+    };
+    if (!pin || pin->hi <= pin->lo) return copy2d(0, rows, false);
     // first row starting at or after lo, first row ending after hi
     size_t r1 = pin->lo <= s0 ? 0 : (size_t)((pin->lo - s0 + spitch - 1) / spitch);
     size_t r2 = pin->hi < s0 + width ? 0 : (size_t)((pin->hi - s0 - width) / spitch) + 1;
@@ -694,7 +753,8 @@ hipError_t upload_rows(const HostPin* pin, uint8_t* dst, size_t dpitch, const ui
         const uintptr_t cuts[4] = {a, std::min(std::max(pin->lo, a), b), std::min(std::max(pin->hi, a), b), b};
         for (int k = 0; k < 3 && e == hipSuccess; k++)
             if (cuts[k + 1] > cuts[k])
-                e = hipMemcpyAsync(dst + r * dpitch + (cuts[k] - start(r)), reinterpret_cast<const void*>(cuts[k]),
+                e = hipMemcpyAsync(dst + r * dpitch + (cuts[k] - start(r)),
+                                   k == 1 ? reinterpret_cast<const uint8_t*>(cuts[k]) : pin->outside(cuts[k]),
                                    cuts[k + 1] - cuts[k], hipMemcpyHostToDevice, s);
     };
     auto outside_rows = [&](size_t a, size_t b, uintptr_t cut) {   // rows [a, b); one may straddle cut
@@ -706,13 +766,13 @@ hipError_t upload_rows(const HostPin* pin, uint8_t* dst, size_t dpitch, const ui
             } else {
                 size_t q = r + 1;   // a run of rows that do not straddle
                 while (q < b && !(start(q) < cut && start(q) + width > cut)) q++;
-                e = copy2d(r, q);
+                e = copy2d(r, q, false);
                 r = q;
             }
         }
     };
     outside_rows(0, r1, pin->lo);
-    if (e == hipSuccess) e = copy2d(r1, r2);
+    if (e == hipSuccess) e = copy2d(r1, r2, true);
     if (e == hipSuccess) outside_rows(r2, rows, pin->hi);
     return e;
 }
@@ -1034,6 +1094,8 @@ void dcte_destroy(dcte_ctx* ctx)
         if (d.down) (void)hipStreamDestroy(d.down);
         if (d.stream) (void)hipStreamDestroy(d.stream);
     }
+    for (auto& st : ctx->stage)
+        if (st.p) (void)hipHostFree(st.p);
     delete ctx;
 }
 
@@ -1728,8 +1790,8 @@ int dcte_energy_map(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, siz
     DCTE_ARG(ctx, rowstride >= (size_t)w * bpp);
     ctx->last_refined = 0;
     const bool one = ctx->devs.size() == 1;
-    HostPin pin_in(ctx, px, (size_t)(h - 1) * rowstride + (size_t)w * bpp);
-    HostPin pin_out(ctx, out, sizeof(float) * (size_t)w * (size_t)h, one && ctx->d2h_kernel);
+    HostPin pin_in(ctx, px, (size_t)(h - 1) * rowstride + (size_t)w * bpp, false, 0, false);
+    HostPin pin_out(ctx, out, sizeof(float) * (size_t)w * (size_t)h, one && ctx->d2h_kernel, 1, true);
     int G = 0;
     int rc;
     if (transposed && one) {   // chunked: the map's download overlaps its launches
@@ -1744,7 +1806,9 @@ int dcte_energy_map(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, siz
         drain(ctx, G);              // nothing in flight may still use px / out
         return rc;
     }
-    return sync_bands(ctx, G);
+    rc = sync_bands(ctx, G);
+    if (rc == DCTE_OK) pin_out.commit();
+    return rc;
 }
 
 int dcte_energy_map2(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, size_t rowstride,
@@ -1764,16 +1828,21 @@ int dcte_energy_map2(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp, si
         return rc;
     }
     ctx->last_refined = 0;
-    HostPin pin_in(ctx, px, (size_t)(h - 1) * rowstride + (size_t)w * bpp);
-    HostPin pin_out(ctx, out, out ? sizeof(float) * (size_t)w * (size_t)h : 0, ctx->d2h_kernel);
-    HostPin pin_out_t(ctx, out_t, out_t ? sizeof(float) * (size_t)w * (size_t)h : 0, ctx->d2h_kernel);
+    HostPin pin_in(ctx, px, (size_t)(h - 1) * rowstride + (size_t)w * bpp, false, 0, false);
+    HostPin pin_out(ctx, out, out ? sizeof(float) * (size_t)w * (size_t)h : 0, ctx->d2h_kernel, 1, true);
+    HostPin pin_out_t(ctx, out_t, out_t ? sizeof(float) * (size_t)w * (size_t)h : 0, ctx->d2h_kernel, 2, true);
     int rc = map_pipeline_one(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, out, out_t,
                               &pin_in, &pin_out, &pin_out_t);
     if (rc) {
         drain(ctx, 1);              // nothing in flight may still use px / out / out_t
         return rc;
     }
-    return sync_bands(ctx, 1);
+    rc = sync_bands(ctx, 1);
+    if (rc == DCTE_OK) {
+        pin_out.commit();
+        pin_out_t.commit();
+    }
+    return rc;
 }
 
 int dcte_energy_image_u8(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp,
@@ -1786,9 +1855,9 @@ int dcte_energy_image_u8(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp
     DCTE_ARG(ctx, rowstride >= (size_t)w * bpp && valid_norm(mode, channels));
     ctx->last_refined = 0;
     int G = 0;
-    HostPin pin_in(ctx, px, (size_t)(h - 1) * rowstride + (size_t)w * bpp);
+    HostPin pin_in(ctx, px, (size_t)(h - 1) * rowstride + (size_t)w * bpp, false, 0, false);
     HostPin pin_out(ctx, out, (size_t)w * (size_t)h * (size_t)channels,
-                    ctx->devs.size() == 1 && ctx->d2h_kernel);
+                    ctx->devs.size() == 1 && ctx->d2h_kernel, 1, true);
     int rc = map_bands(ctx, px, w, h, bpp, rowstride, n, edges, textures, semantics, 0, nullptr,
                        &G, &pin_in);
     if (rc == DCTE_OK) rc = normalize_bands(ctx, w, h, mode, channels, out, G, &pin_out);
@@ -1796,7 +1865,9 @@ int dcte_energy_image_u8(dcte_ctx* ctx, const uint8_t* px, int w, int h, int bpp
         drain(ctx, G);              // nothing in flight may still use px / out
         return rc;
     }
-    return sync_bands(ctx, G);
+    rc = sync_bands(ctx, G);
+    if (rc == DCTE_OK) pin_out.commit();
+    return rc;
 }
 
 }  // extern "C"

@@ -81,10 +81,13 @@ extern "C" {
 #define DCTE_OPT_PROFILE 2 /* 1 = bracket every map-kernel launch with HIP
                               events on its stream (dcte_profile_read) */
 #define DCTE_OPT_PIN_HOST 3 /* host entry points: page-lock the caller's frame
-                               and output for the duration of a call when they
-                               are at least this many MiB (default 1; 0 = never),
-                               so the chunked H2D / D2H copies overlap (pageable
-                               copies are staged serially by the runtime) */
+                               and output (their whole pages) for the duration
+                               of a call when they are at least this many MiB
+                               (default 1; 0 = never), so the chunked H2D / D2H
+                               copies overlap; the bytes no lock covers (partial
+                               end pages, smaller buffers) are staged through a
+                               page-locked buffer of the context -- no copy
+                               takes the runtime's pageable path */
 #define DCTE_OPT_TILE_H 4   /* output rows per map workgroup (0 = the kernel's
                                default, 128); results do not depend on it */
 #define DCTE_OPT_DP_BANDWISE 5 /* 1 = run the seam search one launch per band of

@@ -707,6 +707,40 @@ def test_host_buffers_sharing_pages(ctx):
         assert np.array_equal(px, img)
 
 
+def test_host_staging_multi_device_shared_pages(ctx):
+    """Several devices of one context (the same GPU here) on host frames that
+    are small (staged whole through the context's page-locked arena) and large
+    (whole pages registered, the partial end pages staged), the frame and the
+    map carved from ONE allocation so they share a page, both orientations and
+    u8 layers: equal to the single-device results.  No copy of these calls
+    takes the runtime's pageable path -- r06's fault: the band uploads of a
+    multi-device context, or its transposed strips, copied overlapping pageable
+    pages on several streams at once (test_exact_multi_device_host_path,
+    profiles/r06/multi_device_pageable_fault.log)."""
+    rng = np.random.default_rng(11)
+    with dctenergy.Context(ngpus=3, same_device=True) as many:
+        for h, w in ((700, 301), (2100, 301), (1500, 1031)):
+            img = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+            img[:, ::5] //= 9
+            fb, ob = img.nbytes, 4 * h * w
+            buf = np.zeros(fb + ob + 3 * 4096, np.uint8)
+            off = (-buf.ctypes.data) % 4096 + 100           # the frame starts mid-page ...
+            o_out = off + fb + (-(off + fb + buf.ctypes.data)) % 4   # ... the map on its last page
+            frame = buf[off:off + fb].reshape(h, w, 3)
+            frame[...] = img
+            out = buf[o_out:o_out + ob].view(np.float32).reshape(h, w)
+            for n in (8, 16):
+                ref = ctx.energy_map(img, n, 0.3, 0.7)
+                for c in (ctx, many):
+                    out[...] = -1
+                    assert np.array_equal(c.energy_map(frame, n, 0.3, 0.7, out=out), ref), (h, w, n)
+                    assert np.array_equal(c.energy_map(frame, n, 0.3, 0.7, transposed=True),
+                                          ctx.energy_map(img, n, 0.3, 0.7, transposed=True)), (h, w, n)
+                    assert np.array_equal(c.energy_image_u8(frame, n, 0.3, 0.7, dctenergy.DCTE_NORM_PREVIEW, 3),
+                                          ctx.energy_image_u8(img, n, 0.3, 0.7, dctenergy.DCTE_NORM_PREVIEW, 3))
+            assert np.array_equal(frame, img)
+
+
 @pytest.mark.parametrize("n", [2, 4, 8, 16])
 def test_tile_height_does_not_change_results(n):
     """DCTE_OPT_TILE_H only re-partitions the work: any tile height gives the
