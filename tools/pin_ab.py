@@ -2,13 +2,14 @@
 (DCTE_OPT_PIN_HOST moved from 64 MiB to 1 MiB in r05; the A/B
 then covered only 2048^2 and 4096^2).  For 1-8 MiB frames -- 1024x768 up to
 1920x1080 RGB, what GIMP layers usually are -- times dcte_energy_map with the
-threshold at 0 (never page-lock: the runtime stages the copies), 1 MiB (the
+threshold at 0 (never page-lock: r05 the runtime staged the copies; since
+r06 the library stages every byte through its page-locked arena), 1 MiB (the
 default) and 64 MiB (r04), with the SAME numpy buffers reused across calls
 and with FRESH buffers every call (a new rgb buffer per carver build, as
 init_carver_from_vals allocates, src/render.c:159-173).  One JSON line per
 (size, threshold, buffers): median / best ms over `iters` calls.
 
-    python tools/pin_ab.py
+    python tools/pin_ab.py [HxW ...]
 """
 import json
 import os
@@ -24,7 +25,8 @@ def main():
     import dctenergy
     iters = 15
     rng = np.random.default_rng(0)
-    sizes = [(768, 1024), (1024, 1280), (1080, 1920), (1536, 2048)]
+    sizes = [tuple(int(v) for v in a.split("x")) for a in sys.argv[1:]] or \
+        [(768, 1024), (1024, 1280), (1080, 1920), (1536, 2048)]
     with dctenergy.Context(ngpus=1) as ctx:
         for h, w in sizes:
             base = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
