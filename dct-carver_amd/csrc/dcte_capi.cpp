@@ -1013,10 +1013,17 @@ int sync_bands(dcte_ctx* ctx, int G)
 {
     for (int k = 0; k < G; k++) {
         Device& d = ctx->devs[k];
-        DCTE_HIP(ctx, hipSetDevice(d.id));
-        if (d.up) DCTE_HIP(ctx, hipStreamSynchronize(d.up));
-        DCTE_HIP(ctx, hipStreamSynchronize(d.stream));
-        if (d.down) DCTE_HIP(ctx, hipStreamSynchronize(d.down));
+        hipError_t e = hipSetDevice(d.id);
+        if (e == hipSuccess && d.up) e = hipStreamSynchronize(d.up);
+        if (e == hipSuccess) e = hipStreamSynchronize(d.stream);
+        if (e == hipSuccess && d.down) e = hipStreamSynchronize(d.down);
+        if (e != hipSuccess) {
+            // the caller's buffers are unpinned on return: nothing of this
+            // call may still be in flight on any device
+            const int rc = hip_fail(ctx, e, "sync_bands");
+            drain(ctx, G);
+            return rc;
+        }
         auto it = d.fix.find(d.stream);
         if (it != d.fix.end()) {
             unsigned cnt = 0;
