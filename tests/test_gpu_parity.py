@@ -741,6 +741,34 @@ def test_host_staging_multi_device_shared_pages(ctx):
             assert np.array_equal(frame, img)
 
 
+def test_caller_pinned_views(ctx):
+    """A frame and a map that lie INSIDE the caller's page-locked allocations
+    (torch pin_memory), at odd offsets: used as they are (their device
+    addresses from hipHostGetDevicePointer at the view's offset, no
+    registration, no staging), on one device and on three -- equal to the
+    same calls on ordinary numpy arrays."""
+    import torch
+    rng = np.random.default_rng(12)
+    h, w = 900, 1201
+    img = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+    img[::3] //= 11
+    big = torch.empty(img.nbytes + 1000, dtype=torch.uint8, pin_memory=True).numpy()
+    frame = big[333:333 + img.nbytes].reshape(h, w, 3)
+    frame[...] = img
+    mbuf = torch.empty(2 * h * w + 7, dtype=torch.float32, pin_memory=True).numpy()
+    with dctenergy.Context(ngpus=3, same_device=True) as many:
+        for n in (8, 16):
+            ref = ctx.energy_map(img, n, 0.3, 0.7)
+            reft = ctx.energy_map(img, n, 0.3, 0.7, transposed=True)
+            for c in (ctx, many):
+                out = mbuf[3:3 + h * w].reshape(h, w)
+                out[...] = -1
+                assert np.array_equal(c.energy_map(frame, n, 0.3, 0.7, out=out), ref), n
+                out_t = mbuf[5 + h * w:5 + 2 * h * w].reshape(w, h)
+                assert np.array_equal(c.energy_map(frame, n, 0.3, 0.7, transposed=True, out=out_t), reft), n
+    assert np.array_equal(frame, img)
+
+
 @pytest.mark.parametrize("n", [2, 4, 8, 16])
 def test_tile_height_does_not_change_results(n):
     """DCTE_OPT_TILE_H only re-partitions the work: any tile height gives the
