@@ -289,6 +289,37 @@ def host_path_vertical(ctx, frame_dev, n, e, t, iters=3):
                     f"streams from pinned buffers; two_calls = the r05 glue's two dcte_energy_map calls"}
 
 
+def time_calls(ctx, call, st, iters, rounds):
+    """-> (call_ms, map_ms, call_ms_with_events): the stream time per call in
+    rounds WITHOUT the profiling events (r06: the two events DCTE_OPT_PROFILE
+    records around each map launch cost a 4096^2 call ~6 us of its ~0.1 ms,
+    which r05 counted as refinement), the map launches alone from rounds WITH
+    them (HIP events around each), and those rounds' call time; best of
+    `rounds` interleaved rounds of `iters` calls each."""
+    import torch
+    import dctenergy
+    best_call, best_map, best_ev = 1e9, 1e9, 1e9
+    for _ in range(rounds):
+        for prof in (0, 1):
+            ctx.profile_read()
+            ctx.set_option(dctenergy.DCTE_OPT_PROFILE, prof)
+            a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a0.record(st)
+            for _ in range(iters):
+                call()
+            a1.record(st)
+            torch.cuda.synchronize()
+            ctx.set_option(dctenergy.DCTE_OPT_PROFILE, 0)
+            launches, kms = ctx.profile_read()
+            ms = a0.elapsed_time(a1) / iters
+            if prof:
+                best_ev = min(best_ev, ms)
+                best_map = min(best_map, kms / max(1, launches))
+            else:
+                best_call = min(best_call, ms)
+    return best_call, best_map, best_ev
+
+
 def stress(ctx, n, S, e, t, dev, stream, iters=10, rounds=3):
     """The worst realistic frame for the fp64 tie refinement, timed like the
     headline after it: line-art RGB (black lines on white every 23 rows, every
@@ -296,8 +327,9 @@ def stress(ctx, n, S, e, t, dev, stream, iters=10, rounds=3):
     Its edge/texture ties are exact in real arithmetic (src/dct.c:100-109), so
     the reference's rounding decides them and ~2.7 % of the pixels go through
     the fp64 refinement.  map_ms: the map launches alone (HIP events around
-    each); call_ms: map + refinement (HIP events on the stream); best of
-    `rounds` rounds of `iters` calls."""
+    each); call_ms: map + refinement (HIP events on the stream, rounds without
+    the per-launch events: time_calls); best of `rounds` rounds of `iters`
+    calls."""
     import torch
     import dctenergy
     yy = torch.arange(S, device=dev).view(-1, 1)
@@ -313,21 +345,7 @@ def stress(ctx, n, S, e, t, dev, stream, iters=10, rounds=3):
     for _ in range(2):
         call()
     torch.cuda.synchronize()
-    best_call, best_map = 1e9, 1e9
-    st = torch.cuda.current_stream(dev)
-    for _ in range(rounds):
-        ctx.profile_read()
-        ctx.set_option(dctenergy.DCTE_OPT_PROFILE, 1)
-        a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a0.record(st)
-        for _ in range(iters):
-            call()
-        a1.record(st)
-        torch.cuda.synchronize()
-        ctx.set_option(dctenergy.DCTE_OPT_PROFILE, 0)
-        _, kms = ctx.profile_read()
-        best_call = min(best_call, a0.elapsed_time(a1) / iters)
-        best_map = min(best_map, kms / iters)
+    best_call, best_map, _ = time_calls(ctx, call, torch.cuda.current_stream(dev), iters, rounds)
     # flagged count: the host entry point reports it (same kernels)
     host = fr.cpu().numpy()
     ctx.energy_map(host, n, e, t)
@@ -354,7 +372,9 @@ def other_configs(ctx, e, t, dev, stream, iters=20, rounds=3):
     N = 16) on this GPU, timed like the headline after it, on the same kind of
     synthetic natural-like frame: call_ms = map + refinement per call (HIP
     events on the stream; the headline's step), map_ms = the map launches
-    alone (HIP events around each); best of `rounds` rounds of `iters`."""
+    alone (HIP events around each), call_ms_with_events = the call in the
+    rounds that record those events (time_calls); best of `rounds` rounds of
+    `iters`."""
     import torch
     import dctenergy
     from dctenergy import synth
@@ -370,22 +390,10 @@ def other_configs(ctx, e, t, dev, stream, iters=20, rounds=3):
         for _ in range(3):
             call()
         torch.cuda.synchronize()
-        best_call, best_map = 1e9, 1e9
-        for _ in range(rounds):
-            ctx.profile_read()
-            ctx.set_option(dctenergy.DCTE_OPT_PROFILE, 1)
-            a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a0.record(st)
-            for _ in range(iters):
-                call()
-            a1.record(st)
-            torch.cuda.synchronize()
-            ctx.set_option(dctenergy.DCTE_OPT_PROFILE, 0)
-            launches, kms = ctx.profile_read()
-            best_call = min(best_call, a0.elapsed_time(a1) / iters)
-            best_map = min(best_map, kms / max(1, launches))
+        best_call, best_map, best_ev = time_calls(ctx, call, st, iters, rounds)
         res[key] = {"frame": f"{S}x{S} RGB natural-like, N={n}, e={e}, t={t}",
                     "call_ms": round(best_call, 4), "map_ms": round(best_map, 4),
+                    "call_ms_with_events": round(best_ev, 4), "call_over_map": round(best_call / best_map, 4),
                     "value": round(S * S / best_call / 1e3, 1), "unit": "Mpx/s",
                     "hbm_frac_of_map": round(S * S * 7 / (best_map * 1e-3) / 8.0e12, 4)}
         del fr, out
