@@ -533,9 +533,7 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
             return fail(e, "hipEventCreate");
         }
         ctx->prof.push_back(ev);      // dcte_profile_read destroys them
-        if ((e = hipEventRecord(ev.a, s)) != hipSuccess) return fail(e, "hipEventRecord");
-        if ((e = dcte::launch_map(n, bpp, sem, p, s)) != hipSuccess) return fail(e, "launch_map");
-        if ((e = hipEventRecord(ev.b, s)) != hipSuccess) return fail(e, "hipEventRecord");
+        if ((e = dcte::launch_map(n, bpp, sem, p, s, ev.a, ev.b)) != hipSuccess) return fail(e, "launch_map");
     } else if ((e = dcte::launch_map(n, bpp, sem, p, s)) != hipSuccess) {
         return fail(e, "launch_map");
     }

@@ -169,7 +169,9 @@ struct DpParams {
 };
 
 // host-side launchers (dcte_kernels.hip)
-hipError_t launch_map(int n, int bpp, int sem, const MapParams& p, hipStream_t s);
+// ev_a / ev_b (or null): events the launch records at the kernel's start / end
+hipError_t launch_map(int n, int bpp, int sem, const MapParams& p, hipStream_t s, hipEvent_t ev_a = nullptr,
+                      hipEvent_t ev_b = nullptr);
 hipError_t launch_fix(const FixParams& p, hipStream_t s);
 hipError_t launch_fix_tiles(int n, int bpp, int sem, const TileFixParams& p, hipStream_t s);
 hipError_t launch_seam_carve(const SeamParams& p, hipStream_t s);

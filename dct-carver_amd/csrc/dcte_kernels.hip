@@ -25,6 +25,7 @@
 //  * Pixels whose edge/texture decision falls inside the fp32 error band are
 //    appended to a list and recomputed by dcte_fix in fp64, in the
 //    reference's operation order.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -2396,37 +2397,54 @@ int map_blocks_per_cu(int n, int bpp, int sem)
     }
 }
 
+// With ev_a / ev_b (DCTE_OPT_PROFILE), the launch itself records the kernel's
+// start and end (hipExtLaunchKernel: timestamps of the dispatch, no marker
+// packets of their own -- two hipEventRecord calls around the launch cost a
+// 4096^2 call ~6 us, r06)
 template <int N, int BPP, int SEM>
-static hipError_t launch_map_t(const MapParams& p, hipStream_t s)
+static hipError_t launch_map_t(const MapParams& p, hipStream_t s, hipEvent_t ev_a, hipEvent_t ev_b)
 {
     constexpr int TW = Geo<N, SEM>::TW;
     dim3 grid((p.w + TW - 1) / TW, p.tiles_y);
+    if (ev_a || ev_b) {
+        MapParams arg = p;
+        void* args[] = {&arg};
+        return hipExtLaunchKernel(reinterpret_cast<const void*>(&dcte_map<N, BPP, SEM>), grid,
+                                  dim3(Geo<N, SEM>::T), args, 0, s, ev_a, ev_b, 0);
+    }
     hipLaunchKernelGGL((dcte_map<N, BPP, SEM>), grid, dim3(Geo<N, SEM>::T), 0, s, p);
     return hipGetLastError();
 }
 
 template <int N>
-static hipError_t launch_map_n(int bpp, int sem, const MapParams& p, hipStream_t s)
+static hipError_t launch_map_n(int bpp, int sem, const MapParams& p, hipStream_t s, hipEvent_t a, hipEvent_t b)
 {
     if (sem == kSemLqr) {
-        if (bpp == 1) return launch_map_t<N, 1, kSemLqr>(p, s);
-        if (bpp == 3) return launch_map_t<N, 3, kSemLqr>(p, s);
+        if (bpp == 1) return launch_map_t<N, 1, kSemLqr>(p, s, a, b);
+        if (bpp == 3) return launch_map_t<N, 3, kSemLqr>(p, s, a, b);
     } else if (sem == kSemPreview) {
-        if (bpp == 1) return launch_map_t<N, 1, kSemPreview>(p, s);
-        if (bpp == 3) return launch_map_t<N, 3, kSemPreview>(p, s);
-        if (bpp == 4) return launch_map_t<N, 4, kSemPreview>(p, s);
+        if (bpp == 1) return launch_map_t<N, 1, kSemPreview>(p, s, a, b);
+        if (bpp == 3) return launch_map_t<N, 3, kSemPreview>(p, s, a, b);
+        if (bpp == 4) return launch_map_t<N, 4, kSemPreview>(p, s, a, b);
     }
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_map(int n, int bpp, int sem, const MapParams& p, hipStream_t s)
+hipError_t launch_map(int n, int bpp, int sem, const MapParams& p, hipStream_t s, hipEvent_t ev_a,
+                      hipEvent_t ev_b)
 {
-    if (p.tiles_y <= 0) return hipSuccess;
+    if (p.tiles_y <= 0) {
+        // nothing to launch: the events still mark this point of the stream
+        hipError_t e = hipSuccess;
+        if (ev_a) e = hipEventRecord(ev_a, s);
+        if (e == hipSuccess && ev_b) e = hipEventRecord(ev_b, s);
+        return e;
+    }
     switch (n) {
-    case 2: return launch_map_n<2>(bpp, sem, p, s);
-    case 4: return launch_map_n<4>(bpp, sem, p, s);
-    case 8: return launch_map_n<8>(bpp, sem, p, s);
-    case 16: return launch_map_n<16>(bpp, sem, p, s);
+    case 2: return launch_map_n<2>(bpp, sem, p, s, ev_a, ev_b);
+    case 4: return launch_map_n<4>(bpp, sem, p, s, ev_a, ev_b);
+    case 8: return launch_map_n<8>(bpp, sem, p, s, ev_a, ev_b);
+    case 16: return launch_map_n<16>(bpp, sem, p, s, ev_a, ev_b);
     default: return hipErrorInvalidValue;
     }
 }
