@@ -78,8 +78,9 @@ extern "C" {
                               derived worst-case fp32 error, DESIGN.md §5;
                               a negative value restores these defaults;
                               0 = never refine, >= 1 = refine every pixel) */
-#define DCTE_OPT_PROFILE 2 /* 1 = bracket every map-kernel launch with HIP
-                              events on its stream (dcte_profile_read) */
+#define DCTE_OPT_PROFILE 2 /* 1 = time every map-kernel launch: HIP events
+                              the launch itself records at the kernel's start
+                              and end (dcte_profile_read) */
 #define DCTE_OPT_PIN_HOST 3 /* host entry points: page-lock the caller's frame
                                and output (their whole pages) for the duration
                                of a call when they are at least this many MiB
