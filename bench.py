@@ -361,6 +361,9 @@ def stress(ctx, n, S, e, t, dev, stream, iters=10, rounds=3):
                     f"best of {rounds} rounds of {iters} device calls (HIP events)"}
 
 
+# timed steps between two whose map launches record their start / end (main)
+PROF_EVERY = 5
+
 # fp64 VALU operations per output pixel of the exact kernels (dcte_exact.hip):
 # the reference's own ops (ddct8x8s / ddct16x16s / ddct2d, no FMA), the scan's
 # maxima and the decision per output pixel (idle halo lanes included), counted
@@ -638,20 +641,28 @@ def main():
         step()
     torch.cuda.synchronize()
     ctx.profile_read()
-    ctx.set_option(dctenergy.DCTE_OPT_PROFILE, 1)
+    # the map launches of every PROF_EVERY-th timed step record their start /
+    # end (DCTE_OPT_PROFILE): those events cost a step 2.8 us at 16384^2 but
+    # 6.9 us (3.9 %) on a 2048-row band (interior + edge launch), which would
+    # bend the scaling curve (tools/prof_overhead.py, profiles/r06/prof_overhead.jsonl)
+    profiled = 0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        prof = i % PROF_EVERY == 0
+        ctx.set_option(dctenergy.DCTE_OPT_PROFILE, 1 if prof else 0)
+        profiled += prof
         step()
     enqueued = time.perf_counter() - t0       # host time to issue the K steps
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    launches, kern_ms = ctx.profile_read()
     ctx.set_option(dctenergy.DCTE_OPT_PROFILE, 0)
+    launches, kern_ms = ctx.profile_read()
+    kern_ms = kern_ms / max(1, profiled) * args.steps   # per-step average x K
     stats = torch.tensor([elapsed, kern_ms / args.steps, enqueued], dtype=torch.float64,
                          device="cpu" if gloo else dev)
     per_rank_kernel_ms = [kern_ms / args.steps]
@@ -793,6 +804,7 @@ def main():
                 "algorithmic_bytes_per_px": 7,
                 "px_per_rank": px_per_rank,
                 "launches_timed": launches,
+                "steps_profiled": f"{profiled} of {args.steps} (every {PROF_EVERY}th timed step)",
                 "note": "rank 0's map launches; binding roof is VALU (see valu) -- the HBM "
                         "fraction this computation can reach is bounded by its VALU op count "
                         "(N=8: ~24 %; DESIGN.md §4)",
