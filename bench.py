@@ -191,6 +191,37 @@ def cpu_baseline(frame_rows_host, W, n, e, t, sample_rows):
     return res
 
 
+def link_floor(px_pin, d_px, downs, dev, iters):
+    """-> (floor_s, up_s, down_s, both_s): median times of the frame's H2D
+    alone, the maps' D2H alone and both at once on two streams, pinned
+    buffers.  floor = max(up, down): no call can move these bytes faster,
+    whatever engines it uses (r06: on some boxes the runtime serialises an
+    SDMA upload with an SDMA download, so `both` is not a floor -- the library
+    downloads through a copy kernel and beats it)."""
+    import torch
+    s_up, s_down = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def med(up, down):
+        ts = []
+        for _ in range(iters + 1):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            if up:
+                with torch.cuda.stream(s_up):
+                    d_px.copy_(px_pin, non_blocking=True)
+            if down:
+                with torch.cuda.stream(s_down):
+                    for dst, src in downs:
+                        dst.copy_(src, non_blocking=True)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        ts = sorted(ts[1:])
+        return ts[len(ts) // 2]
+
+    up, down, both = med(True, False), med(False, True), med(True, True)
+    return max(up, down), up, down, both
+
+
 def host_path(ctx, frame_dev, n, e, t, iters=3):
     """The plug-in's own call: a pageable host frame (GIMP's rgb buffer,
     src/render.c:159-173) -> dcte_energy_map -> a pageable host map; the library
@@ -207,32 +238,24 @@ def host_path(ctx, frame_dev, n, e, t, iters=3):
         ts.append(time.perf_counter() - t0)
     ts.sort()
     med = ts[len(ts) // 2]
-    # the floor: the same bytes both ways at once (pinned buffers, two streams)
+    # the floor: each direction alone from pinned buffers, full duplex assumed
     import torch
     px_pin = torch.empty(tuple(px.shape), dtype=torch.uint8, pin_memory=True)
     out_pin = torch.empty((H, W), dtype=torch.float32, pin_memory=True)
     d_px = torch.empty(tuple(px.shape), dtype=torch.uint8, device=frame_dev.device)
     d_out = torch.empty((H, W), dtype=torch.float32, device=frame_dev.device)
-    s_up, s_down = torch.cuda.Stream(frame_dev.device), torch.cuda.Stream(frame_dev.device)
-    fl = []
-    for _ in range(iters + 1):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        with torch.cuda.stream(s_up):
-            d_px.copy_(px_pin, non_blocking=True)
-        with torch.cuda.stream(s_down):
-            out_pin.copy_(d_out, non_blocking=True)
-        torch.cuda.synchronize()
-        fl.append(time.perf_counter() - t0)
-    floor = sorted(fl[1:])[len(fl[1:]) // 2]
+    floor, up, down, both = link_floor(px_pin, d_px, [(out_pin, d_out)], frame_dev.device, iters)
     del px_pin, out_pin, d_px, d_out
     return {"value": round(H * W / med / 1e9, 2), "unit": "Gpx/s", "ms": round(med * 1e3, 2),
             "best_ms": round(ts[0] * 1e3, 2), "iters": iters,
             "bytes_h2d": int(px.nbytes), "bytes_d2h": int(out.nbytes),
             "duplex_floor_ms": round(floor * 1e3, 2), "frac_of_floor": round(floor / med, 3),
+            "h2d_alone_ms": round(up * 1e3, 2), "d2h_alone_ms": round(down * 1e3, 2),
+            "sdma_both_ms": round(both * 1e3, 2),
             "what": f"{H}x{W} RGB pageable host frame -> dcte_energy_map -> host map "
-                    f"(PCIe-inclusive; page-locked per call, chunk pipeline); floor = the frame's "
-                    f"H2D and the map's D2H at once on two streams from pinned buffers"}
+                    f"(PCIe-inclusive; page-locked per call, chunk pipeline); floor = max(the frame's "
+                    f"H2D alone, the map's D2H alone) from pinned buffers; sdma_both = both copies at "
+                    f"once on two streams (torch, copy engines)"}
 
 
 def host_path_vertical(ctx, frame_dev, n, e, t, iters=3):
@@ -265,28 +288,20 @@ def host_path_vertical(ctx, frame_dev, n, e, t, iters=3):
     out_pin2 = torch.empty((W, H), dtype=torch.float32, pin_memory=True)
     d_px = torch.empty(tuple(px.shape), dtype=torch.uint8, device=frame_dev.device)
     d_out = torch.empty((H, W), dtype=torch.float32, device=frame_dev.device)
-    s_up, s_down = torch.cuda.Stream(frame_dev.device), torch.cuda.Stream(frame_dev.device)
-    fl = []
-    for _ in range(iters + 1):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        with torch.cuda.stream(s_up):
-            d_px.copy_(px_pin, non_blocking=True)
-        with torch.cuda.stream(s_down):
-            out_pin.copy_(d_out, non_blocking=True)
-            out_pin2.view(H, W).copy_(d_out, non_blocking=True)
-        torch.cuda.synchronize()
-        fl.append(time.perf_counter() - t0)
-    floor = sorted(fl[1:])[len(fl[1:]) // 2]
+    floor, up, down, both = link_floor(px_pin, d_px, [(out_pin, d_out), (out_pin2.view(H, W), d_out)],
+                                       frame_dev.device, iters)
     del px_pin, out_pin, out_pin2, d_px, d_out
     return {"value": round(H * W / med / 1e9, 2), "unit": "Gpx/s (frame pixels, both maps)",
             "ms": round(med * 1e3, 2), "best_ms": round(ts[0] * 1e3, 2), "iters": iters,
             "two_calls_ms": round(two_calls * 1e3, 2),
             "bytes_h2d": int(px.nbytes), "bytes_d2h": int(2 * out.nbytes),
             "duplex_floor_ms": round(floor * 1e3, 2), "ratio_to_floor": round(med / floor, 3),
+            "h2d_alone_ms": round(up * 1e3, 2), "d2h_alone_ms": round(down * 1e3, 2),
+            "sdma_both_ms": round(both * 1e3, 2),
             "what": f"{H}x{W} RGB pageable host frame -> dcte_energy_map2 -> both maps on the host "
-                    f"(one upload; PCIe-inclusive); floor = one H2D and two D2H at once on two "
-                    f"streams from pinned buffers; two_calls = the r05 glue's two dcte_energy_map calls"}
+                    f"(one upload; PCIe-inclusive); floor = max(one H2D alone, two D2H alone) from "
+                    f"pinned buffers; sdma_both = all three copies at once on two streams (torch); "
+                    f"two_calls = the r05 glue's two dcte_energy_map calls"}
 
 
 def time_calls(ctx, call, st, iters, rounds):
@@ -394,9 +409,18 @@ def other_configs(ctx, e, t, dev, stream, iters=20, rounds=3):
             call()
         torch.cuda.synchronize()
         best_call, best_map, best_ev = time_calls(ctx, call, st, iters, rounds)
+        # the same call with the refinement off (tie_tau = 0: the map launch
+        # alone) -- what one launch costs beyond its kernel, so call_ms minus
+        # this is the refinement launch's own cost
+        ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, 0.0)
+        one_call, _, _ = time_calls(ctx, call, st, iters, rounds)
+        ctx.set_option(dctenergy.DCTE_OPT_TIE_TAU, -1.0)
         res[key] = {"frame": f"{S}x{S} RGB natural-like, N={n}, e={e}, t={t}",
                     "call_ms": round(best_call, 4), "map_ms": round(best_map, 4),
                     "call_ms_with_events": round(best_ev, 4), "call_over_map": round(best_call / best_map, 4),
+                    "one_launch_call_ms": round(one_call, 4),
+                    "one_launch_over_map": round(one_call / best_map, 4),
+                    "refinement_launch_ms": round(best_call - one_call, 4),
                     "value": round(S * S / best_call / 1e3, 1), "unit": "Mpx/s",
                     "hbm_frac_of_map": round(S * S * 7 / (best_map * 1e-3) / 8.0e12, 4)}
         del fr, out

@@ -492,6 +492,14 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     p.tiles_a = tiles_a;
     p.tiles_y = tiles_y;
     p.fair = fair;
+    // N = 8 launches of fewer than DCTE_EPI_MAX_PX output pixels refine their
+    // sparse strips inside the map launch (dcte_map's epilogue): on a natural
+    // 1024^2 / 2048^2 / 4096^2 frame the call is 8 / 5 / 2-3 % shorter (the
+    // separate launch's sparse walk, a chain of dependent loads, is most of
+    // that launch's cost); 6144^2 and 8192^2 even; at 16384^2 the tiles holding
+    // a wave for their epilogue cost the map 1.2 % more than that walk
+    // (profiles/r06/map_epi_ab.jsonl)
+    p.epi = (long long)w * (rows_a + rows_b) < dcte::kEpiMaxPx ? 1 : 0;
     p.out = d_out;
     p.out_stride = out_stride;
     p.we = (float)((double)edges / scale);
@@ -504,6 +512,7 @@ int run_device(dcte_ctx* ctx, Device& d, const void* d_px, long long rowstride, 
     p.dirty_list = f->d_tiles + ntiles;
     p.dirty_count = f->d_count + 2 + f->phase;
     p.dirty_next = f->d_count + 2 + (f->phase ^ 1u);
+    p.fix_total = f->d_count + 1;
     p.dense_ctr = reinterpret_cast<unsigned long long*>(f->d_count + 4) + f->phase;
     p.dense_next = reinterpret_cast<unsigned long long*>(f->d_count + 4) + (f->phase ^ 1u);
     p.dense_list = reinterpret_cast<uint2*>(f->d_tiles + 2 * ntiles);

@@ -79,50 +79,7 @@ __device__ __forceinline__ double weight(bool edge, double we, double wt)
 
 using r64::K8;
 
-// Pass 2 of ddct8x8s on coefficient row k1 (shrtdct.c:90-117: a[k1][0..7] ->
-// C_k1,0..7), folded into the scan's maxima.  v[j] = a[k1][j] after pass 1.
-//   ROLE 0 (k1 = 0): a01 = |C01|, m0 = max |C0,2..7| (C00 is never scanned)
-//   ROLE 1 (k1 = 1): a10 = |C10| (into a01's slot), mp = max(mp, |C1,1..7|)
-//   ROLE 2 (k1 >= 2): mp = max(mp, |C_k1,0..7|)
-template <int ROLE>
-__device__ __forceinline__ void col8(double v0, double v1, double v2, double v3, double v4, double v5,
-                                     double v6, double v7, double& a, double& m)
-{
-    const double x0r = v0 + v7, x1r = v0 - v7;
-    const double x0i = v2 + v5, x1i = v2 - v5;
-    const double x2r = v4 + v3, x3r = v4 - v3;
-    const double x2i = v6 + v1, x3i = v6 - v1;
-    double xr = x0r + x2r, xi = x0i + x2i;
-    double acc;
-    if constexpr (ROLE == 0) {
-        acc = fabs(K8::c4 * (xr - xi));                       // C04
-    } else if constexpr (ROLE == 1) {
-        a = fabs(K8::c4 * (xr + xi));                          // C10
-        acc = fmax(m, fabs(K8::c4 * (xr - xi)));               // C14
-    } else {
-        acc = fmax(m, K8::c4 * (fabs(xr) + fabs(xi)));         // max(|C_k1,0|, |C_k1,4|)
-    }
-    xr = x0r - x2r;
-    xi = x0i - x2i;
-    acc = fmax(acc, fabs(K8::c2 * xr - K8::s2 * xi));          // C_k1,2
-    acc = fmax(acc, fabs(K8::c2 * xi + K8::s2 * xr));          // C_k1,6
-    xr = K8::w4 * (x1i - x3i);
-    const double y1i = K8::w4 * (x1i + x3i);
-    const double y3i = y1i - x3r;
-    const double z1i = y1i + x3r;
-    const double y3r = x1r - xr;
-    const double y1r = x1r + xr;
-    const double c1 = K8::c1 * y1r - K8::s1 * z1i;             // C_k1,1
-    if constexpr (ROLE == 0) {
-        a = fabs(c1);
-    } else {
-        acc = fmax(acc, fabs(c1));
-    }
-    acc = fmax(acc, fabs(K8::c1 * z1i + K8::s1 * y1r));        // C_k1,7
-    acc = fmax(acc, fabs(K8::c3 * y3r - K8::s3 * y3i));        // C_k1,3
-    acc = fmax(acc, fabs(K8::c3 * y3i + K8::s3 * y3r));        // C_k1,5
-    m = acc;
-}
+using r64::col8;
 
 // Frame bytes through one bounds-checked buffer resource over the readable
 // rows (a dword straddling the end reads as 0: the <= 3 tail bytes are fetched

@@ -17,6 +17,13 @@ namespace dcte {
 // window clamp can touch for the output rows (clamp(y0 - N/2 + 1) ..
 // clamp(last - 1 + N/2)) must be readable: a row band plus its halo, or the
 // whole frame.
+// N = 8 map launches below this many output pixels refine their sparse strips
+// themselves (MapParams::epi)
+#ifndef DCTE_EPI_MAX_PX
+#define DCTE_EPI_MAX_PX 25000000LL
+#endif
+constexpr long long kEpiMaxPx = DCTE_EPI_MAX_PX;
+
 struct MapParams {
     const uint8_t* px;
     long long rowstride;     // bytes
@@ -27,6 +34,7 @@ struct MapParams {
     int tile_h;              // output rows per workgroup
     int tiles_a, tiles_y;    // tile rows of [y0, y1); of the launch
     int fair;                // > 0: priority levels a workgroup steps down through its tile
+    int epi;                 // N = 8: the launch refines its own sparse strips (small launches)
     float* out;              // row y at out + (y - y0) * out_stride
     long long out_stride;    // floats
     float we, wt;            // edges / textures weights, pre-scaled to luma units
@@ -43,6 +51,7 @@ struct MapParams {
     unsigned* dirty_list;
     unsigned* dirty_count;   // zero when the launch starts
     unsigned* dirty_next;    // zeroed by this launch: the next launch's dirty_count
+    unsigned* fix_total;     // pixels refined (N = 8: the map's own sparse strips; null: none)
     // N = 8 (and N = 16 liblqr): the DENSE strips (more than kFixDirect flags)
     // once more, as one flat work list for the dense refinement walks
     // (fix_dense16_flat): *dense_ctr = {strips << 32 | entries}

@@ -65,6 +65,9 @@ namespace dcte {
 #ifndef DCTE_TSTAMP
 #define DCTE_TSTAMP 0      // timing-probe builds: per-workgroup timestamps (tools/tstamp.py)
 #endif
+#ifndef DCTE_MAP_EPI
+#define DCTE_MAP_EPI 1   // N = 8: the map launch refines its own sparse strips (r06)
+#endif
 #ifndef DCTE_PF2_MAXN
 #define DCTE_PF2_MAXN 4    // N <= this: raw rows prefetched two groups ahead (else one)
 #endif
@@ -139,6 +142,62 @@ __device__ __forceinline__ void static_for(F&& f)
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+// forward declarations (refinement section below)
+template <int N, class Line>
+__device__ __forceinline__ void refine_group_f(Line&& line, double* w, int l, double& best, bool& edge);
+
+// N = 8: the sparse strips of a map tile refined by the map launch itself,
+// after its last row (a small frame's call paid a second
+// launch for a few hundred flagged pixels).  Wave w owns strip w of the tile
+// (cnt flagged pixels at el[0 .. cnt), cnt <= kFixDirect: the rest go to
+// dcte_fix_strips as before).  Four pixels per pass, one 8-lane group each
+// (lanes 32-63 repeat lanes 0-31's pixels: same values into the same LDS);
+// the window gathered from the frame with the replicate clamp of
+// src/render.c:146-152, liblqr luma in double [liblqr, unverified] / the
+// preview's RGB2LUMINANCE, ddct8x8s and the last-maximum scan in the
+// reference's order (refine_group_f) -- the bits dcte_fix_strips produces.
+// lds: the map's luma buffer, free after its last barrier (>= 256 + waves x
+// 4 x 72 doubles).  Every thread of the workgroup calls it.
+template <int N, int BPP, int SEM>
+__device__ __forceinline__ void map_refine_sparse(const MapParams& p, double* lds, unsigned cnt,
+                                                  const unsigned* el, int sx0, int ys, int tx, int nthreads)
+{
+    constexpr int HL = Geo<N, SEM>::HL;
+    double* const lut = lds;                         // v / 255 (liblqr)
+    for (int v = tx; v < 256; v += nthreads) lut[v] = (double)v / 255;
+    __syncthreads();
+    if (cnt - 1u >= (unsigned)kFixDirect<N>) return;   // uniform per wave: nothing, or dcte_fix_strips'
+    const int lane = tx & 63, l = lane & (N - 1), grp = (lane / N) & 3;
+    double* const w = lds + 256 + ((tx >> 6) * 4 + grp) * (N * (N + 1));
+    auto luma = [&](const uint8_t* q) -> double {
+        if constexpr (SEM == kSemLqr) {
+            if constexpr (BPP == 1) return lut[q[0]];
+            else return 0.2126 * lut[q[0]] + 0.7152 * lut[q[1]] + 0.0722 * lut[q[2]];
+        } else {
+            return (double)preview_luma(q[0], BPP > 1 ? q[1] : 0u, BPP > 1 ? q[2] : 0u, BPP);
+        }
+    };
+    for (unsigned e0 = 0; e0 < cnt; e0 += 4) {       // uniform
+        const unsigned e = e0 + (unsigned)grp;
+        const bool valid = e < cnt;
+        const unsigned loc = el[valid ? e : 0u];
+        const int x = sx0 + (int)(loc & 63u), y = ys + (int)(loc >> 6);
+        double best;
+        bool edge;
+        // lane l: liblqr data[i][l] = pixel (x - HL + i, y - HL + l); preview
+        // data[i][l] = data[dy = i][dx = l]
+        refine_group_f<N>([&](int i) {
+            const int ox = SEM == kSemLqr ? i : l, oy = SEM == kSemLqr ? l : i;
+            const int gx = clampi(x - HL + ox, 0, p.w - 1), gy = clampi(y - HL + oy, 0, p.h - 1);
+            return luma(p.px + (long long)(gy - p.in_row0) * p.rowstride + (long long)gx * BPP);
+        }, w, l, best, edge);
+        if (valid && l == 0 && lane < 32)
+            p.out[(long long)(y - p.y0) * p.out_stride + x] =
+                edge ? (float)(best * (double)p.edges) : (float)(best * (double)p.textures);
+    }
+    if (p.fix_total && lane == 0) atomicAdd(p.fix_total, cnt);
+}
+
 // ------------------------------------------------------------------ main kernel
 template <int N, int BPP, int SEM>
 __global__ __launch_bounds__((Geo<N, SEM>::T), MapThreads<N>::min_waves) void dcte_map(const MapParams p)
@@ -165,7 +224,7 @@ __global__ __launch_bounds__((Geo<N, SEM>::T), MapThreads<N>::min_waves) void dc
     constexpr bool kDirectLds = S == 1 && kDB && !kPF2 &&
                                 LW - kThreads > 0 && (LW - kThreads) * G <= 64;
     __shared__ uint32_t raw[kDirectLds ? 1 : NB][kDirectLds ? 1 : G][kDirectLds ? 1 : NDW];
-    __shared__ float lum[NB][G][LWP];
+    __shared__ __attribute__((aligned(16))) float lum[NB][G][LWP];
     // S = 4 (N = 16): the group's rows' maxima over the four waves, met by
     // LDS atomic max on the bits (non-negative floats order as their bits);
     // only the waves owning k1 = 0 (q = 0) and k1 = 1 (q = 2) carry an edge
@@ -177,6 +236,12 @@ __global__ __launch_bounds__((Geo<N, SEM>::T), MapThreads<N>::min_waves) void dc
     // refinement lists per 64-column strip (one wave's columns; N = 16: the tile)
     constexpr int SPT = S == 1 ? TW / 64 : 1;        // strips per tile
     __shared__ unsigned nflag[SPT];                  // pixels each strip flagged
+    // N = 8: a strip with at most kFixDirect flagged pixels is refined by its
+    // own wave after the last row (map_refine_sparse), not by dcte_fix_strips;
+    // its entries are kept here as well
+    constexpr bool kEpi = N == 8 && S == 1 && DCTE_MAP_EPI;
+    constexpr unsigned kEpiMax = kFixDirect<N>;
+    __shared__ unsigned elist[kEpi ? SPT : 1][kEpi ? kEpiMax : 1];
 
     const int tx = threadIdx.x;
     const int lane_p = (S == 4) ? (tx >> 6) : 0;     // N = 16: wave index = k1 class
@@ -382,7 +447,10 @@ __global__ __launch_bounds__((Geo<N, SEM>::T), MapThreads<N>::min_waves) void dc
         // pixel when tie_tau >= 1 (testing)
         if (inside && ((check_ties && me > keep * mt && mt > keep * me) || force_all)) {
             const unsigned k = atomicAdd(&nflag[sc], 1u);      // < 64 * tile_h
-            strip_list[k] = (unsigned)((y - ys) * 64 + (xx - sx0));
+            const unsigned loc = (unsigned)((y - ys) * 64 + (xx - sx0));
+            strip_list[k] = loc;
+            if constexpr (kEpi)
+                if (k < kEpiMax) elist[sc][k] = loc;   // (read only when p.epi)
         }
     };
 
@@ -586,9 +654,21 @@ __global__ __launch_bounds__((Geo<N, SEM>::T), MapThreads<N>::min_waves) void dc
         }
     }
     __syncthreads();
+    bool epi = false;                                // uniform
+    if constexpr (kEpi) {
+        epi = p.epi != 0;
+        bool any = false;                            // uniform over the workgroup
+#pragma unroll
+        for (int s2 = 0; s2 < SPT; s2++) any = any || (nflag[s2] - 1u < kEpiMax);
+        if (epi && any) {
+            static_assert(sizeof(lum) >= sizeof(double) * (256 + SPT * 4 * N * (N + 1)), "epilogue LDS");
+            map_refine_sparse<N, BPP, SEM>(p, reinterpret_cast<double*>(&lum[0][0][0]), nflag[sc], elist[sc],
+                                           sx0, ys, tx, kThreads);
+        }
+    }
     if (tx < SPT) {
         const unsigned cnt = nflag[tx];
-        if (cnt) {
+        if (cnt && !(epi && cnt <= kEpiMax)) {
             const unsigned st = strip - sc + tx;
             p.tile_count[st] = cnt;
             p.dirty_list[atomicAdd(p.dirty_count, 1u)] = st;
@@ -716,6 +796,12 @@ __device__ __forceinline__ void lastmax_group(const double* v, int l, double& m,
 // registers (N <= 8): ddct8x8s along the first index, then the second;
 // ddct2d (N = 2, 4) the second index first.  The scan keeps the LAST maximum
 // (src/dct.c:103, "max <= currval"); edge atoms (0,1), (1,0) (src/dct.c:18-25).
+#ifndef DCTE_GREY_ACC
+#define DCTE_GREY_ACC 1  // N = 4, 8 RGB lane walk: one grey test per window (rgb_grey_acc, r06)
+#endif
+#ifndef DCTE_FIX_COL8
+#define DCTE_FIX_COL8 1  // N = 8: pass 2 through r64::col8 (r06)
+#endif
 #ifndef DCTE_FIX_IL
 #define DCTE_FIX_IL 1    // N = 8 register path: 8-point steps the scheduler may interleave
 #endif
@@ -730,11 +816,29 @@ __device__ __forceinline__ void refine_regs(double (&d)[N * N], const double* ct
             r64::step8(d + i, 8);
             if ((i + 1) % IL == 0) __builtin_amdgcn_sched_barrier(0);
         }
+        // pass 2 folded into the scan (r64::col8: step8's operations on row
+        // k1 in its order, C00 never formed, max(|C_k1,0|, |C_k1,4|) as one
+        // exact product for k1 >= 2 -- the exact maps' form, bit-identical)
+#if DCTE_FIX_COL8
+        double a01, a10, mb, ma = -1.0;
+        r64::col8<0>(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7], a01, mb);
+        r64::col8<1>(d[8], d[9], d[10], d[11], d[12], d[13], d[14], d[15], a10, ma);
+#pragma unroll
+        for (int i = 2; i < 8; i++) {
+            double unused;
+            r64::col8<2>(d[8 * i], d[8 * i + 1], d[8 * i + 2], d[8 * i + 3], d[8 * i + 4], d[8 * i + 5],
+                         d[8 * i + 6], d[8 * i + 7], unused, ma);
+            if ((i + 1) % IL == 0) __builtin_amdgcn_sched_barrier(0);
+        }
+        lastmax_decide(a01, a10, mb, ma, m, edge);
+        return;
+#else
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             r64::step8(d + 8 * i, 1);
             if ((i + 1) % IL == 0) __builtin_amdgcn_sched_barrier(0);
         }
+#endif
     } else {
 #pragma unroll
         for (int i = 0; i < N; i++) r64::step_small(N, d + N * i, 1, ct);
@@ -1019,6 +1123,24 @@ __device__ __forceinline__ bool rgb_line_grey(const uint32_t (&wd)[K])
     return acc == 0u;
 }
 
+// The same test over a whole window, cheaper: the lines' differences are
+// OR-ed per dword class (j mod 3) across all lines and masked once at the end
+// (6 + 6 + 3 operations per 8-pixel line instead of 24)
+template <int K>
+__device__ __forceinline__ void rgb_grey_acc(const uint32_t (&wd)[K], uint32_t (&acc)[3])
+{
+    static_assert(K % 3 == 0, "whole pixels: 4 per 3 dwords");
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+        const uint32_t nx = __builtin_amdgcn_alignbyte(j < K - 1 ? wd[j + 1] : 0u, wd[j], 1u);
+        acc[j % 3] |= wd[j] ^ nx;
+    }
+}
+__device__ __forceinline__ bool rgb_grey_done(const uint32_t (&acc)[3])
+{
+    return ((acc[0] & 0xFF00FFFFu) | (acc[1] & 0xFFFF00FFu) | (acc[2] & 0x00FFFF00u)) == 0u;
+}
+
 // Window memo of the dense lane walks, N = 4 and 8 (r04).  Tie-dense frames are regular:
 // their flagged windows repeat (straight strokes, grid lines, flat fills, the
 // same glyph), and a window's refined energy depends only on its bytes.  Each
@@ -1210,15 +1332,36 @@ __device__ __forceinline__ void fix_dense_lane(const TileFixParams& tp, const do
         // liblqr -- or the same u8 luma -- preview) instead of three
         bool grey = false;
         if constexpr (BPP == 3) {
-            bool mine = true;
+            bool all_fast = true;
+#pragma unroll
+            for (int rr = 0; rr < N; rr++) all_fast = all_fast && fast[rr];
+#if DCTE_GREY_ACC
+            // the first row alone first: a colour window on any lane ends the
+            // test for the wave there (uniform branch)
+            auto acc_row = [&](int rr, uint32_t (&acc)[3]) {
+                uint32_t wd[3 * KW];
+#pragma unroll
+                for (int j = 0; j < 3 * KW; j++) wd[j] = wa[rr][j];
+                rgb_grey_acc(wd, acc);
+            };
+            uint32_t acc[3] = {0u, 0u, 0u};
+            acc_row(0, acc);
+            if (__all(all_fast && rgb_grey_done(acc))) {     // uniform
+#pragma unroll
+                for (int rr = 1; rr < N; rr++) acc_row(rr, acc);
+                grey = __all(rgb_grey_done(acc));          // uniform
+            }
+#else
+            bool mine = all_fast;
 #pragma unroll
             for (int rr = 0; rr < N; rr++) {
                 uint32_t wd[3 * KW];
 #pragma unroll
                 for (int j = 0; j < 3 * KW; j++) wd[j] = wa[rr][j];
-                mine = mine && fast[rr] && rgb_line_grey(wd);
+                mine = mine && rgb_line_grey(wd);
             }
-            grey = __all(mine);                  // uniform
+            grey = __all(mine);
+#endif
         }
         double d[N * N];
         const int gx0 = x - HL;
