@@ -398,7 +398,10 @@ def other_configs(ctx, e, t, dev, stream, iters=20, rounds=3):
     from dctenergy import synth
     res = {}
     st = torch.cuda.current_stream(dev)
-    for S, n, key in ((4096, 8, "config2_4096_rgb_n8"), (8192, 16, "config5_8192_rgb_n16")):
+    # (plus a 2048^2 layer, the size GIMP users carve most: the per-call costs
+    # weigh most there)
+    for S, n, key in ((4096, 8, "config2_4096_rgb_n8"), (8192, 16, "config5_8192_rgb_n16"),
+                      (2048, 8, "layer_2048_rgb_n8")):
         fr = synth.natural_rows(0, S, S, 3, seed=0, device=dev)
         out = torch.empty((S, S), dtype=torch.float32, device=dev)
 
@@ -427,8 +430,8 @@ def other_configs(ctx, e, t, dev, stream, iters=20, rounds=3):
         if n == 16:                    # the N = 16 tie-dense worst case beside it
             res[key]["stress"] = stress(ctx, 16, S, e, t, dev, stream)
     torch.cuda.empty_cache()
-    res["what"] = ("BASELINE configs[1] and configs[4] after the timed region (the headline is "
-                   "configs[2]); call = map + tie refinement, as the headline's step")
+    res["what"] = ("BASELINE configs[1] and configs[4] (and a 2048^2 layer) after the timed region "
+                   "(the headline is configs[2]); call = map + tie refinement, as the headline's step")
     return res
 
 
