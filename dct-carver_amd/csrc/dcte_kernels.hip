@@ -65,9 +65,6 @@ namespace dcte {
 #ifndef DCTE_TSTAMP
 #define DCTE_TSTAMP 0      // timing-probe builds: per-workgroup timestamps (tools/tstamp.py)
 #endif
-#ifndef DCTE_MAP_EPI
-#define DCTE_MAP_EPI 1   // N = 8: the map launch refines its own sparse strips (r06)
-#endif
 #ifndef DCTE_PF2_MAXN
 #define DCTE_PF2_MAXN 4    // N <= this: raw rows prefetched two groups ahead (else one)
 #endif
@@ -239,7 +236,7 @@ __global__ __launch_bounds__((Geo<N, SEM>::T), MapThreads<N>::min_waves) void dc
     // N = 8: a strip with at most kFixDirect flagged pixels is refined by its
     // own wave after the last row (map_refine_sparse), not by dcte_fix_strips;
     // its entries are kept here as well
-    constexpr bool kEpi = N == 8 && S == 1 && DCTE_MAP_EPI;
+    constexpr bool kEpi = N == 8 && S == 1;
     constexpr unsigned kEpiMax = kFixDirect<N>;
     __shared__ unsigned elist[kEpi ? SPT : 1][kEpi ? kEpiMax : 1];
 
@@ -796,12 +793,6 @@ __device__ __forceinline__ void lastmax_group(const double* v, int l, double& m,
 // registers (N <= 8): ddct8x8s along the first index, then the second;
 // ddct2d (N = 2, 4) the second index first.  The scan keeps the LAST maximum
 // (src/dct.c:103, "max <= currval"); edge atoms (0,1), (1,0) (src/dct.c:18-25).
-#ifndef DCTE_GREY_ACC
-#define DCTE_GREY_ACC 1  // N = 4, 8 RGB lane walk: one grey test per window (rgb_grey_acc, r06)
-#endif
-#ifndef DCTE_FIX_COL8
-#define DCTE_FIX_COL8 1  // N = 8: pass 2 through r64::col8 (r06)
-#endif
 #ifndef DCTE_FIX_IL
 #define DCTE_FIX_IL 1    // N = 8 register path: 8-point steps the scheduler may interleave
 #endif
@@ -818,8 +809,8 @@ __device__ __forceinline__ void refine_regs(double (&d)[N * N], const double* ct
         }
         // pass 2 folded into the scan (r64::col8: step8's operations on row
         // k1 in its order, C00 never formed, max(|C_k1,0|, |C_k1,4|) as one
-        // exact product for k1 >= 2 -- the exact maps' form, bit-identical)
-#if DCTE_FIX_COL8
+        // exact product for k1 >= 2 -- the exact maps' form, bit-identical;
+        // line art RGB -1.4 %, profiles/r06/refine_col8_grey_ab.jsonl)
         double a01, a10, mb, ma = -1.0;
         r64::col8<0>(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7], a01, mb);
         r64::col8<1>(d[8], d[9], d[10], d[11], d[12], d[13], d[14], d[15], a10, ma);
@@ -832,13 +823,6 @@ __device__ __forceinline__ void refine_regs(double (&d)[N * N], const double* ct
         }
         lastmax_decide(a01, a10, mb, ma, m, edge);
         return;
-#else
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            r64::step8(d + 8 * i, 1);
-            if ((i + 1) % IL == 0) __builtin_amdgcn_sched_barrier(0);
-        }
-#endif
     } else {
 #pragma unroll
         for (int i = 0; i < N; i++) r64::step_small(N, d + N * i, 1, ct);
@@ -1335,9 +1319,10 @@ __device__ __forceinline__ void fix_dense_lane(const TileFixParams& tp, const do
             bool all_fast = true;
 #pragma unroll
             for (int rr = 0; rr < N; rr++) all_fast = all_fast && fast[rr];
-#if DCTE_GREY_ACC
-            // the first row alone first: a colour window on any lane ends the
-            // test for the wave there (uniform branch)
+            // one test over the window (rgb_grey_acc), the first row alone
+            // first: a colour window on any lane ends the test for the wave
+            // there (uniform branch) -- line art RGB -2.6 % with col8 below,
+            // colour strokes -2.9 % (profiles/r06/refine_col8_grey_ab.jsonl)
             auto acc_row = [&](int rr, uint32_t (&acc)[3]) {
                 uint32_t wd[3 * KW];
 #pragma unroll
@@ -1351,17 +1336,6 @@ __device__ __forceinline__ void fix_dense_lane(const TileFixParams& tp, const do
                 for (int rr = 1; rr < N; rr++) acc_row(rr, acc);
                 grey = __all(rgb_grey_done(acc));          // uniform
             }
-#else
-            bool mine = all_fast;
-#pragma unroll
-            for (int rr = 0; rr < N; rr++) {
-                uint32_t wd[3 * KW];
-#pragma unroll
-                for (int j = 0; j < 3 * KW; j++) wd[j] = wa[rr][j];
-                mine = mine && rgb_line_grey(wd);
-            }
-            grey = __all(mine);
-#endif
         }
         double d[N * N];
         const int gx0 = x - HL;

@@ -32,9 +32,7 @@ KNOBS = {
     "DCTE_FIX_DIRECT8": ("dcte_kernels.hip", "128u"),
     "DCTE_FIX_DIRECT4": ("dcte_kernels.hip", "64u"),
     "DCTE_FIX_IL": ("dcte_kernels.hip", "2"),
-    "DCTE_FIX_COL8": ("dcte_kernels.hip", "0"),
-    "DCTE_GREY_ACC": ("dcte_kernels.hip", "0"),
-    "DCTE_MAP_EPI": ("dcte_kernels.hip", "0"),
+    "DCTE_EPI_MAX_PX": ("dcte_capi.cpp", "0LL"),
     "DCTE_FIX_GPS": ("dcte_kernels.hip", "1"),
     "DCTE_FIX_MINW": ("dcte_kernels.hip", "3"),
     "DCTE_FIX_MINW_LANES": ("dcte_kernels.hip", "3"),
